@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Benchmark of the PF hot path (one "step" = one PF frame: propagate + weight + resample) on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
+
+N = 1 runs BASELINE.json configs[1] (C2: 5 LEDs, 100k particles, 50 blobs/frame, fp32 state).  For N > 1
+the driver launches one process per GPU with torch.distributed.run; every rank runs an INDEPENDENT camera
+stream (its own seed) on its own GPU — the path shards across streams with no data-path collective
+(SURVEY.md §8e), so scaling is "weak".  gloo (CPU) carries only the barrier and the max-over-ranks time.
+
+Inputs are resident in HBM before the timed region (pfmpe_stage_blob_bank); each step calls pfmpe_step,
+which is blocking (its last act is the stream synchronize that brings the winner to the host), so the
+timed region is bracketed by barrier + device sync on both sides.
+
+Extra objects on the JSON line:
+  roofline     — dominant kernel's algorithmic bytes per launch / its HIP-event-timed average duration
+  cpu_baseline — the oracle (single-thread restatement of the reference loop, O(N^2) resample) timed on
+                 this host on a bounded sample of the same workload (rank 0, N = 1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4"])
+    ap.add_argument("--particles", type=int, default=0, help="override N")
+    ap.add_argument("--force-iters", type=int, default=0)
+    ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
+    ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
+    ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    return ap.parse_args()
+
+
+def algorithmic_bytes(S: int, N: int) -> dict:
+    """Compulsory HBM bytes per launch (DESIGN.md "Roofline")."""
+    return {
+        "k_propagate_weigh": N * (S + 4),      # read prior state, write weight
+        "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
+        "k_iter_reduce": 0, "k_prep": 0, "k_final": 0,
+    }
+
+
+def cpu_baseline(cfg, n_frames: int):
+    from oracle import pforacle as orc
+    from pf_monocular_pose_estimator_amd import synthetic as syn
+    st = syn.make_stream(cfg, n_frames)
+    prior = st.prior()
+    times, iters = [], []
+    for fr in st.frames:
+        t0 = time.perf_counter()
+        out, arr = orc.pf_step(st.markers, st.K, orc.make_params(), prior, fr.current_pose, fr.predicted_pose,
+                               fr.prediction, fr.blobs, dt=fr.dt, seed=11 + fr.index, frame_idx=fr.index)
+        times.append(time.perf_counter() - t0)
+        iters.append(out["iters"])
+        if out["resampled"]:
+            prior = arr["resampled"]
+    tm = statistics.median(times)
+    k = statistics.median(iters)
+    return {
+        "value": cfg.N * k / tm, "unit": "particle-updates/s", "cores": 1, "kind": "port",
+        "sample": f"{n_frames} frames of {cfg.name} (N={cfg.N}, M={cfg.M}, B={cfg.B}); oracle/pf_oracle.cpp "
+                  f"fp64, median {tm:.3f} s/frame, k={k}; single thread like the reference's ros::spin",
+    }
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo on CPU: barrier + max only
+        dist.init_process_group("gloo")
+
+    import pf_monocular_pose_estimator_amd as pf
+    from pf_monocular_pose_estimator_amd import synthetic as syn
+
+    base = syn.CONFIGS[args.config]
+    cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=args.particles or base.N, heavy=base.heavy, seed=rank)
+    n_frames = args.warmup + args.steps
+    st = syn.make_stream(cfg, n_frames)
+    eng = pf.Engine(device=local_rank, max_particles=cfg.N, state_dtype=pf.STATE_F32)
+    eng.set_model(st.markers, st.K)
+    prm = pf.default_params()
+    prm.rng_mode = pf.RNG_PHILOX if args.rng == "philox" else pf.RNG_REFERENCE
+    eng.set_params(prm)
+    eng.set_prior(st.prior())
+    eng.stage_blob_bank([f.blobs for f in st.frames])
+    frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
+                             dt=f.dt, seed=(rank << 32) + 17 + f.index, frame_idx=f.index,
+                             force_iters=args.force_iters) for f in st.frames]
+
+    for i in range(args.warmup):
+        eng.step(frames[i])
+    eng.reset_kernel_stats()
+    if not args.no_timing:
+        eng.set_option(pf.OPT_TIMING, 1)
+
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    updates = 0
+    accepted = 0
+    iters = []
+    for i in range(args.warmup, n_frames):
+        out = eng.step(frames[i])  # blocking: ends with the stream synchronize
+        updates += cfg.N * out.iters
+        iters.append(out.iters)
+        accepted += out.accepted
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    stats = eng.kernel_stats()
+    eng.set_option(pf.OPT_TIMING, 0)
+
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        u = torch.tensor([updates], dtype=torch.float64)
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        total_updates = float(u.item())
+    else:
+        total_updates = float(updates)
+
+    if rank == 0:
+        S = 48  # fp32 SoA state bytes per particle
+        ab = algorithmic_bytes(S, cfg.N)
+        roof = None
+        timed = {k: v for k, v in stats.items() if v[0] > 0}
+        if timed:
+            dom = max(timed, key=lambda k: timed[k][1])
+            launches, ms = timed[dom]
+            avg_s = ms / 1e3 / launches
+            achieved = ab.get(dom, 0) / avg_s / 1e9 if avg_s > 0 else 0.0
+            roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "bytes_per_launch": ab.get(dom, 0), "avg_us": round(avg_s * 1e6, 3),
+                    "per_kernel_avg_us": {k: round(v[1] * 1e3 / v[0], 3) for k, v in timed.items()}}
+        cpu = None
+        if world == 1 and args.cpu_frames > 0:
+            cpu = cpu_baseline(cfg, args.cpu_frames)
+        k_mean = float(np.mean(iters)) if iters else 0.0
+        line = {
+            "metric": "particle-updates/sec (propagate+weight+resample) per GPU; frames/sec at N_particles",
+            "value": total_updates / elapsed,
+            "unit": "particle-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{cfg.name}: {cfg.M} LEDs, {cfg.N} particles, {cfg.B} blobs/frame, fp32 SoA state "
+                            f"(BASELINE.json configs[1])" if cfg.name == "C2" else f"{cfg.name}",
+                "N_particles": cfg.N, "markers": cfg.M, "blobs": cfg.B,
+                "frames_per_sec_per_gpu": args.steps / elapsed,
+                "iters_per_frame": k_mean, "accept_rate": accepted / max(1, args.steps),
+                "rng": args.rng, "parallelism": f"{world} independent camera streams (1 per GPU), no collectives",
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/*
+ * pfmpe.h — C-ABI of the MI355X particle-filter pose engine (the drop-in boundary).
+ *
+ * The reference has no function/plugin boundary around its PF step: the step is ~200 inline lines in
+ * PoseEstimator::estimateBodyPose (pf_mpe_lib/src/pose_estimator.cpp:475-733, "PE" below) sharing ~15
+ * member fields (pf_mpe_lib/include/pf_mpe_lib/pose_estimator.h:65-169).  This header cuts it at the
+ * PE:535 seam: the host keeps detection, prediction (predictPose PE:995), initialisation and Gauss-Newton
+ * (PE:1805) and replaces PE:475-733 with one pfmpe_step() call.  Each entry point below cites the
+ * reference state or code it replaces.  Plain C types only — no HIP/torch types cross the boundary.
+ *
+ * Conventions
+ *   - Poses are 12 doubles: the top 3 rows of the homogeneous 4x4, row-major:
+ *       [r00 r01 r02 t0  r10 r11 r12 t1  r20 r21 r22 t2]   (the Eigen::Matrix4d of the reference).
+ *   - Blob coordinates are undistorted pixels (image_points_, PE:469 / led_detector.cpp:198-209), B x 2.
+ *   - Return codes: 0 = OK, < 0 = error (PFMPE_E_*); pfmpe_last_error() gives text.  Algorithmic
+ *     outcomes (accept / re-initialise) are NOT errors: see pfmpe_frame_out.flag_fail (reference codes).
+ *   - A context is bound to one HIP device and one HIP stream and is not thread-safe; distinct contexts
+ *     share nothing and may run concurrently (one per camera stream / tracked object / GPU).
+ *   - pfmpe_step() is blocking: it returns after the frame's scalars and winner pose are on the host.
+ *     The resampled particle set stays resident in HBM across frames (newPoseEstimation, PE:681).
+ */
+#ifndef PFMPE_H_
+#define PFMPE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFMPE_ABI_VERSION 1
+#define PFMPE_MAX_MARKERS 16   /* reference bMarkerDowngrade has 5 entries; we take per-marker flags */
+#define PFMPE_MAX_BLOBS 1024
+
+enum {
+  PFMPE_OK = 0,
+  PFMPE_E_ARG = -1,   /* bad argument / size                      */
+  PFMPE_E_HIP = -2,   /* HIP runtime failure (device, alloc, launch) */
+  PFMPE_E_CAP = -3,   /* exceeds the capacity given at create time  */
+  PFMPE_E_STATE = -4  /* call order (e.g. step before set_model)    */
+};
+
+/* particle state storage in HBM (SoA planes) */
+enum { PFMPE_STATE_F32 = 0, PFMPE_STATE_F64 = 1 };
+
+/* motion / resample random streams */
+enum {
+  PFMPE_RNG_REFERENCE = 0, /* std::default_random_engine (minstd_rand0) stream of PE:476-477, 510-523,
+                              reproduced on device by LCG jump-ahead: bit-identical draws */
+  PFMPE_RNG_PHILOX = 1     /* counter-based Philox4x32-10 keyed by (seed, frame, iter, particle) */
+};
+
+/* flag_fail codes (pf_mpe/include/pf_mpe/monocular_pose_estimator.h:121-137, PE:635, PE:711) */
+enum { PFMPE_FLAG_ACCEPTED = 1, PFMPE_FLAG_REINIT = 4 };
+
+typedef struct pfmpe_ctx pfmpe_ctx;
+
+/* PF parameters — the public fields of PoseEstimator (pose_estimator.h:121-155) that the PF block reads,
+ * plus the constants the reference hard-codes (made explicit, defaults = reference values). */
+typedef struct {
+  double tol;        /* back_projection_pixel_tolerance_   score normaliser (PE:2416)           */
+  double tol_pf;     /* back_projection_pixel_tolerance_PF acceptance gate (PE:2414)            */
+  double ang_min;    /* minAngularNoise   (rad)                                                 */
+  double ang_max;    /* maxAngularNoise   (rad)                                                 */
+  double trans_min;  /* minTransitionNoise (m)                                                  */
+  double trans_max;  /* maxTransitionNoise (m)                                                  */
+  double growth;     /* 0.025: noise growth per 10 iterations (PE:563)                          */
+  int32_t max_iter;  /* 80  (PE:616)                                                            */
+  int32_t exit_cap;  /* 5   exit when max w >= M*min(exit_cap, B)   (PE:616)                    */
+  int32_t accept_cap;/* 3   accept when best > M*min(accept_cap, B) (PE:633)                    */
+  int32_t rng_mode;  /* PFMPE_RNG_*                                                             */
+} pfmpe_params;
+
+/* Per-frame host inputs */
+typedef struct {
+  double current_pose[12];   /* current_pose_   -> particle 0 (PE:547)                          */
+  double predicted_pose[12]; /* camMoveInv * predicted_pose_ (PE:395) -> particle 1 (PE:551)    */
+  double prediction[12];     /* predictionMatrix = predictPose() (PE:234, PE:995-1010)          */
+  double cam_move_inv[12];   /* camMoveInv (identity unless bUseCamPos, PE:241-393)             */
+  const double* blobs;       /* B x 2 undistorted px; host pointer (ignored if bank_frame >= 0)  */
+  int32_t B;                 /* numLED (PE:449)                                                 */
+  int32_t bank_frame;        /* -1: use `blobs`; >= 0: frame index in the device blob bank       */
+  int32_t it_since_init;     /* it_since_initialized_ (1 right after init, 2 steady state)      */
+  int32_t force_iters;       /* 0: reference exit rule; > 0: run exactly this many iterations   */
+  double dt;                 /* predicted_time_ - current_time_ (PE:499)                        */
+  uint64_t seed;             /* replaces std::random_device (PE:476); reference mode uses low 32 */
+  uint64_t frame_idx;        /* Philox counter word                                             */
+} pfmpe_frame_in;
+
+/* Per-frame outputs: the scalars the host needs after PE:733 */
+typedef struct {
+  int32_t iters;            /* PF iterations executed (k)                                        */
+  int32_t kept_iter;        /* iteration whose particle set was kept (PE:608-624)                */
+  int32_t most_likely_idx;  /* mostLikelyParticleIdx (PE:610; PE:714 on the re-init branch)      */
+  int32_t accepted;         /* probPartSum != 0 && highestProb > M*min(3,B)  (PE:633)            */
+  int32_t resampled;        /* stratified resampling ran (PE:666-682); new prior is resident     */
+  int32_t winner_idx;       /* argmax resample count (PE:685-686), -1 if not resampled           */
+  int32_t n_corr;           /* rows of correspondences_ for the winner (PE:688)                  */
+  int32_t flag_fail;        /* PFMPE_FLAG_ACCEPTED / PFMPE_FLAG_REINIT                           */
+  double highest_prob;      /* highestProb                                                        */
+  double prob_sum;          /* probPartSum = sum of kept raw weights (PE:627)                     */
+  double winner_pose[12];   /* PoseParticle[winner] -> predicted_pose_ before GN (PE:687);
+                               on re-init: PoseParticle[most_likely_idx] (PE:716)                */
+  double most_likely_pose[12]; /* PoseParticle[most_likely_idx]                                  */
+  uint32_t corr[2 * PFMPE_MAX_MARKERS]; /* (LED, blob) 1-based pairs, extraction order (PE:2417) */
+} pfmpe_frame_out;
+
+/* ---------------------------------------------------------------------------------- lifetime */
+/* Replaces the PoseEstimator member state of pose_estimator.h:65-70 (PoseParticle, newPoseEstimation,
+ * probPart) with device-resident SoA buffers sized for max_particles. */
+int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_markers, int max_blobs,
+                 int state_dtype);
+void pfmpe_destroy(pfmpe_ctx* ctx);
+const char* pfmpe_last_error(const pfmpe_ctx* ctx);
+int pfmpe_abi_version(void);
+
+/* ----------------------------------------------------------------------------------- model/params */
+/* object_points_ (PoseEstimator::setMarkerPositions PE:56), camera_matrix_K_ (3x3 row-major,
+ * monocular_pose_estimator.cpp:215-238) and bMarkerDowngrade (monocular_pose_estimator.cpp:510-517,
+ * here one flag per marker; NULL = none). */
+int pfmpe_set_model(pfmpe_ctx* ctx, const double* markers_xyz, int M, const double* K,
+                    const uint8_t* downgrade);
+/* Fills the PF parameter fields (dynamicParametersCallback, monocular_pose_estimator.cpp:480-527). */
+int pfmpe_set_params(pfmpe_ctx* ctx, const pfmpe_params* params);
+void pfmpe_default_params(pfmpe_params* params);
+
+/* Sets N = N_Particle and the prior newPoseEstimation (N x 12).  Called after (re)initialisation,
+ * which seeds the particle set (PE:1429-1437, 1756-1760). */
+int pfmpe_set_prior(pfmpe_ctx* ctx, const double* poses, int N);
+
+/* ------------------------------------------------------------------------------------- the step */
+/* One PF step = PE:475-690 (+ PE:707-719): propagate, project, weigh (iterating per PE:535-616),
+ * normalise, accept, stratified-resample, pick the winner.  Blocking. */
+int pfmpe_step(pfmpe_ctx* ctx, const pfmpe_frame_in* in, pfmpe_frame_out* out);
+
+/* getPoseParticles (PE:917, which = 0: kept propagated set of the last step) and getResampledParticles
+ * (PE:923, which = 1: current prior).  N x 12 doubles. */
+int pfmpe_get_particles(pfmpe_ctx* ctx, int which, double* out);
+/* probPart of the last step: the kept iteration's raw (un-normalised) weights, N doubles. */
+int pfmpe_get_weights(pfmpe_ctx* ctx, double* out);
+/* counterMeas of the last step (PE:524, 678): N uint32; requires PFMPE_OPT_RECORD_COUNTS. */
+int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
+
+/* Engine options (value semantics in brackets; defaults first):
+ *   PFMPE_OPT_RECORD_COUNTS [0|1]  keep counterMeas on device for pfmpe_get_counts
+ *   PFMPE_OPT_PRUNE         [1|0]  exact x-window blob pruning in the likelihood (0 = scan all B blobs)
+ *   PFMPE_OPT_TIMING        [0|1]  bracket every kernel launch with HIP events (pfmpe_get_kernel_stats) */
+enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3 };
+int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
+
+/* ----------------------------------------------------------------------- device-resident inputs */
+/* Stages a bank of frames' blob lists in HBM (frame f = blobs[offsets[f] .. offsets[f+1]) rows), so a
+ * caller replaying recorded detections (or the benchmark) passes bank_frame instead of host pointers. */
+int pfmpe_stage_blob_bank(pfmpe_ctx* ctx, const double* blobs, const int32_t* offsets, int nframes);
+
+/* ------------------------------------------------------------------------------ instrumentation */
+/* Per-kernel statistics collected while PFMPE_OPT_TIMING is on: launches and summed device time (ms)
+ * measured with HIP events on the ctx stream. */
+enum { PFMPE_K_PREP = 0, PFMPE_K_PROPAGATE = 1, PFMPE_K_REDUCE = 2, PFMPE_K_RESAMPLE = 3,
+       PFMPE_K_FINAL = 4, PFMPE_K_COUNT = 5 };
+int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
+int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
+const char* pfmpe_kernel_name(int kernel);
+
+/* ------------------------------------------------------------------------------ host-side checks */
+/* Pure host functions (no GPU needed): they evaluate the same __host__ __device__ code the kernels use,
+ * so CPU tests can pin RNG/geometry semantics against the oracle without a GPU. */
+/* j-th (0-based) uniform_real_distribution<double>(a,b) draw of a default_random_engine(seed) */
+double pfmpe_host_ref_uniform(uint32_t seed, uint64_t j, double a, double b);
+void pfmpe_host_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFMPE_H_ */

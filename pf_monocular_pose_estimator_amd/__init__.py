@@ -1,0 +1,17 @@
+"""pf_monocular_pose_estimator_amd — MI355X-native particle-filter pose engine.
+
+The hot path of ObiRobotics/pf_monocular_pose_estimator (the PF step of PoseEstimator::estimateBodyPose,
+pf_mpe_lib/src/pose_estimator.cpp:475-733) as hand-written HIP for gfx950 behind the C-ABI in
+include/pfmpe.h.  This package holds the in-tree built library (libpfmpe.so), its ctypes binding
+(`_capi`), and the synthetic stream generator used by tests and bench.py.
+"""
+from ._capi import (  # noqa: F401
+    Engine, FrameIn, FrameOut, Params, PFError, default_params, load, host_philox, host_ref_uniform,
+    STATE_F32, STATE_F64, RNG_REFERENCE, RNG_PHILOX, FLAG_ACCEPTED, FLAG_REINIT,
+    OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, MAX_MARKERS, MAX_BLOBS, LIB_PATH,
+)
+
+__all__ = [
+    "Engine", "FrameIn", "FrameOut", "Params", "PFError", "default_params", "load",
+    "STATE_F32", "STATE_F64", "RNG_REFERENCE", "RNG_PHILOX",
+]

@@ -1,0 +1,266 @@
+"""ctypes binding of the C-ABI in include/pfmpe.h (libpfmpe.so, built in-tree by __graft_entry__.build()).
+
+This is the same boundary a reference-side maintainer would bind; it loads ONLY the
+HIP-built product library and raises if it is missing — there is no CPU fallback on the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpfmpe.so")
+
+MAX_MARKERS = 16
+MAX_BLOBS = 1024
+
+OK, E_ARG, E_HIP, E_CAP, E_STATE = 0, -1, -2, -3, -4
+STATE_F32, STATE_F64 = 0, 1
+RNG_REFERENCE, RNG_PHILOX = 0, 1
+FLAG_ACCEPTED, FLAG_REINIT = 1, 4
+OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING = 1, 2, 3
+K_PREP, K_PROPAGATE, K_REDUCE, K_RESAMPLE, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5
+
+# every symbol include/pfmpe.h declares (tests check the .so exports all of them)
+EXPORTED_SYMBOLS = (
+    "pfmpe_create", "pfmpe_destroy", "pfmpe_last_error", "pfmpe_abi_version",
+    "pfmpe_set_model", "pfmpe_set_params", "pfmpe_default_params", "pfmpe_set_prior",
+    "pfmpe_step", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
+    "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
+    "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
+)
+
+
+class Params(C.Structure):
+    _fields_ = [
+        ("tol", C.c_double), ("tol_pf", C.c_double),
+        ("ang_min", C.c_double), ("ang_max", C.c_double),
+        ("trans_min", C.c_double), ("trans_max", C.c_double),
+        ("growth", C.c_double),
+        ("max_iter", C.c_int32), ("exit_cap", C.c_int32), ("accept_cap", C.c_int32),
+        ("rng_mode", C.c_int32),
+    ]
+
+
+class FrameIn(C.Structure):
+    _fields_ = [
+        ("current_pose", C.c_double * 12), ("predicted_pose", C.c_double * 12),
+        ("prediction", C.c_double * 12), ("cam_move_inv", C.c_double * 12),
+        ("blobs", C.POINTER(C.c_double)), ("B", C.c_int32), ("bank_frame", C.c_int32),
+        ("it_since_init", C.c_int32), ("force_iters", C.c_int32),
+        ("dt", C.c_double), ("seed", C.c_uint64), ("frame_idx", C.c_uint64),
+    ]
+
+
+class FrameOut(C.Structure):
+    _fields_ = [
+        ("iters", C.c_int32), ("kept_iter", C.c_int32), ("most_likely_idx", C.c_int32),
+        ("accepted", C.c_int32), ("resampled", C.c_int32), ("winner_idx", C.c_int32),
+        ("n_corr", C.c_int32), ("flag_fail", C.c_int32),
+        ("highest_prob", C.c_double), ("prob_sum", C.c_double),
+        ("winner_pose", C.c_double * 12), ("most_likely_pose", C.c_double * 12),
+        ("corr", C.c_uint32 * (2 * MAX_MARKERS)),
+    ]
+
+    def pairs(self) -> np.ndarray:
+        return np.array(self.corr[: 2 * self.n_corr], dtype=np.uint32).reshape(-1, 2)
+
+    def as_dict(self) -> dict:
+        return {
+            "iters": self.iters, "kept_iter": self.kept_iter, "most_likely_idx": self.most_likely_idx,
+            "accepted": self.accepted, "resampled": self.resampled, "winner_idx": self.winner_idx,
+            "n_corr": self.n_corr, "flag_fail": self.flag_fail, "highest_prob": self.highest_prob,
+            "prob_sum": self.prob_sum, "winner_pose": np.array(self.winner_pose),
+            "most_likely_pose": np.array(self.most_likely_pose), "pairs": self.pairs(),
+        }
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libpfmpe.so (raises if it has not been built: the product has no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    lib = C.CDLL(LIB_PATH)
+    P, I, D, U64, I64 = C.c_void_p, C.c_int, C.c_double, C.c_uint64, C.c_int64
+    dp = C.POINTER(C.c_double)
+    sig = {
+        "pfmpe_create": (I, [C.POINTER(P), I, I, I, I, I]),
+        "pfmpe_destroy": (None, [P]),
+        "pfmpe_last_error": (C.c_char_p, [P]),
+        "pfmpe_abi_version": (I, []),
+        "pfmpe_set_model": (I, [P, dp, I, dp, C.POINTER(C.c_uint8)]),
+        "pfmpe_set_params": (I, [P, C.POINTER(Params)]),
+        "pfmpe_default_params": (None, [C.POINTER(Params)]),
+        "pfmpe_set_prior": (I, [P, dp, I]),
+        "pfmpe_step": (I, [P, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
+        "pfmpe_get_particles": (I, [P, I, dp]),
+        "pfmpe_get_weights": (I, [P, dp]),
+        "pfmpe_get_counts": (I, [P, C.POINTER(C.c_uint32)]),
+        "pfmpe_set_option": (I, [P, I, I64]),
+        "pfmpe_stage_blob_bank": (I, [P, dp, C.POINTER(C.c_int32), I]),
+        "pfmpe_get_kernel_stats": (I, [P, I, C.POINTER(I64), dp]),
+        "pfmpe_reset_kernel_stats": (I, [P]),
+        "pfmpe_kernel_name": (C.c_char_p, [I]),
+        "pfmpe_host_ref_uniform": (D, [C.c_uint32, U64, D, D]),
+        "pfmpe_host_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def default_params() -> Params:
+    p = Params()
+    load().pfmpe_default_params(C.byref(p))
+    return p
+
+
+def _dptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+class PFError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"pfmpe error {code}: {msg}")
+        self.code = code
+
+
+class Engine:
+    """One PF context (one camera stream / tracked object) on one HIP device."""
+
+    def __init__(self, device: int = 0, max_particles: int = 1000, max_markers: int = MAX_MARKERS,
+                 max_blobs: int = MAX_BLOBS, state_dtype: int = STATE_F32):
+        self.lib = load()
+        self.ctx = C.c_void_p()
+        rc = self.lib.pfmpe_create(C.byref(self.ctx), device, max_particles, max_markers, max_blobs, state_dtype)
+        if rc != OK:
+            raise PFError(rc, "pfmpe_create failed (no HIP device?)")
+        self.state_dtype = state_dtype
+        self.N = 0
+
+    def close(self):
+        if self.ctx:
+            self.lib.pfmpe_destroy(self.ctx)
+            self.ctx = C.c_void_p()
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int):
+        if rc != OK:
+            raise PFError(rc, self.lib.pfmpe_last_error(self.ctx).decode())
+
+    def set_model(self, markers: np.ndarray, K: np.ndarray, downgrade=None):
+        m = np.ascontiguousarray(markers, dtype=np.float64).reshape(-1, 3)
+        k = np.ascontiguousarray(K, dtype=np.float64).reshape(9)
+        dg = None
+        if downgrade is not None:
+            dga = np.ascontiguousarray(downgrade, dtype=np.uint8)
+            dg = dga.ctypes.data_as(C.POINTER(C.c_uint8))
+        self._chk(self.lib.pfmpe_set_model(self.ctx, _dptr(m), m.shape[0], _dptr(k), dg))
+
+    def set_params(self, params: Params):
+        self._chk(self.lib.pfmpe_set_params(self.ctx, C.byref(params)))
+
+    def set_option(self, opt: int, value: int):
+        self._chk(self.lib.pfmpe_set_option(self.ctx, opt, int(value)))
+
+    def set_prior(self, poses: np.ndarray):
+        p = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 12)
+        self._chk(self.lib.pfmpe_set_prior(self.ctx, _dptr(p), p.shape[0]))
+        self.N = p.shape[0]
+
+    def stage_blob_bank(self, frames):
+        offs = np.zeros(len(frames) + 1, dtype=np.int32)
+        for i, f in enumerate(frames):
+            offs[i + 1] = offs[i] + len(f)
+        allb = np.ascontiguousarray(np.concatenate([np.asarray(f, np.float64).reshape(-1, 2) for f in frames]
+                                                   + [np.zeros((0, 2))]), dtype=np.float64)
+        self._bank_keep = allb
+        self._chk(self.lib.pfmpe_stage_blob_bank(self.ctx, _dptr(allb), offs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                 len(frames)))
+
+    @staticmethod
+    def make_frame(current_pose, predicted_pose, prediction, blobs=None, B=None, cam_move_inv=None,
+                   it_since_init=2, dt=0.02, seed=1, frame_idx=0, force_iters=0, bank_frame=-1):
+        fi = FrameIn()
+        fi.current_pose[:] = list(np.asarray(current_pose, np.float64).reshape(12))
+        fi.predicted_pose[:] = list(np.asarray(predicted_pose, np.float64).reshape(12))
+        fi.prediction[:] = list(np.asarray(prediction, np.float64).reshape(12))
+        cm = np.eye(4)[:3].reshape(12) if cam_move_inv is None else np.asarray(cam_move_inv, np.float64).reshape(12)
+        fi.cam_move_inv[:] = list(cm)
+        keep = None
+        if blobs is not None:
+            keep = np.ascontiguousarray(blobs, dtype=np.float64).reshape(-1, 2)
+            fi.blobs = _dptr(keep)
+            fi.B = keep.shape[0]
+        else:
+            fi.blobs = C.POINTER(C.c_double)()
+            fi.B = int(B or 0)
+        fi.bank_frame = bank_frame
+        fi.it_since_init = it_since_init
+        fi.force_iters = force_iters
+        fi.dt = dt
+        fi.seed = seed
+        fi.frame_idx = frame_idx
+        fi._keep = keep  # keep the blob buffer alive with the struct
+        return fi
+
+    def step(self, frame: FrameIn) -> FrameOut:
+        out = FrameOut()
+        self._chk(self.lib.pfmpe_step(self.ctx, C.byref(frame), C.byref(out)))
+        return out
+
+    def get_particles(self, which: int) -> np.ndarray:
+        out = np.empty((self.N, 12), dtype=np.float64)
+        self._chk(self.lib.pfmpe_get_particles(self.ctx, which, _dptr(out)))
+        return out
+
+    def get_weights(self) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.float64)
+        self._chk(self.lib.pfmpe_get_weights(self.ctx, _dptr(out)))
+        return out
+
+    def get_counts(self) -> np.ndarray:
+        out = np.empty(self.N, dtype=np.uint32)
+        self._chk(self.lib.pfmpe_get_counts(self.ctx, out.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return out
+
+    def kernel_stats(self) -> dict:
+        res = {}
+        for k in range(K_COUNT):
+            n = C.c_int64()
+            ms = C.c_double()
+            self._chk(self.lib.pfmpe_get_kernel_stats(self.ctx, k, C.byref(n), C.byref(ms)))
+            res[self.lib.pfmpe_kernel_name(k).decode()] = (n.value, ms.value)
+        return res
+
+    def reset_kernel_stats(self):
+        self._chk(self.lib.pfmpe_reset_kernel_stats(self.ctx))
+
+
+def host_ref_uniform(seed: int, j: int, a: float, b: float) -> float:
+    return load().pfmpe_host_ref_uniform(seed, j, a, b)
+
+
+def host_philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    load().pfmpe_host_philox(c, k, o)
+    return list(o)

@@ -1,0 +1,622 @@
+// pfmpe_engine.hip — host side of the MI355X PF engine: context, buffers, launch sequence, C-ABI.
+//
+// Replaces the PF block of PoseEstimator::estimateBodyPose (pf_mpe_lib/src/pose_estimator.cpp:475-733)
+// behind include/pfmpe.h.  Device layout (DESIGN.md "HBM layout"): particle state as 12 SoA planes
+// (r00 r01 r02 t0 r10 r11 r12 t1 r20 r21 r22 t2) of `ld` elements each, double-buffered (prior /
+// posterior); two weight slots (current iteration / best iteration so far); per-block partials;
+// one control record; one output record copied to pinned host memory at the end of the frame.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/pfmpe.h"
+#include "pf_kernels.hpp"
+
+using namespace pfmpe;
+
+static_assert(sizeof(OutDev) == 8 + sizeof(pfmpe_frame_out), "OutDev must mirror pfmpe_frame_out");
+static_assert(PFMPE_MAX_MARKERS == kMaxMarkers, "marker capacity mismatch");
+static_assert(PFMPE_MAX_BLOBS == kMaxBlobs, "blob capacity mismatch");
+
+struct EventPair {
+  hipEvent_t a, b;
+  int kid;
+};
+
+struct pfmpe_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int max_particles = 0, max_markers = 0, max_blobs = 0, state_dtype = PFMPE_STATE_F32;
+  size_t es = 4;       // bytes per state element
+  int64_t ld = 0;      // plane stride (elements)
+  int max_blk = 0;
+
+  void* d_state[2] = {nullptr, nullptr};
+  int prior_idx = 0;
+  void* d_w[2] = {nullptr, nullptr};
+  BlockPart* d_part[2] = {nullptr, nullptr};
+  double* d_Eb = nullptr;
+  double* d_Rin = nullptr;
+  CountPart* d_cparts = nullptr;
+  void* d_table = nullptr;
+  Ctrl* d_ctrl = nullptr;
+  OutDev* d_out = nullptr;
+  OutDev* h_out = nullptr;       // pinned
+  double* d_blobs = nullptr;
+  double* h_blobs = nullptr;     // pinned staging
+  double* d_bank = nullptr;
+  std::vector<int32_t> bank_off;
+  double* d_xfer = nullptr;      // N x 12 doubles
+  uint32_t* d_counts = nullptr;
+
+  // model / params
+  int M = 0;
+  double markers[kMaxMarkers * 3] = {0};
+  double K[9] = {0};
+  uint32_t downgrade = 0;
+  bool has_model = false;
+  pfmpe_params params{};
+  int N = 0;
+  bool has_prior = false;
+
+  // options
+  bool record_counts = false;
+  bool prune = true;
+  bool timing = false;
+
+  // last step (for get_particles / get_weights)
+  FrameArgs last_fa{};
+  bool has_last = false;
+  int last_prior_idx = 0;
+  bool last_accepted = false;
+
+  // timing
+  std::vector<EventPair> ev_pool;
+  size_t ev_used = 0;
+  int64_t k_launches[PFMPE_K_COUNT] = {0};
+  double k_ms[PFMPE_K_COUNT] = {0};
+
+  std::string err;
+};
+
+namespace {
+
+int fail(pfmpe_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                       \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail((ctx), PFMPE_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+int set_device(pfmpe_ctx* c) {
+  HIPCHK(c, hipSetDevice(c->device));
+  return PFMPE_OK;
+}
+
+// ---------------------------------------------------------------------- timed launch wrapper
+template <typename Launch>
+int launch(pfmpe_ctx* c, int kid, Launch&& fn) {
+  EventPair* ep = nullptr;
+  if (c->timing) {
+    if (c->ev_used == c->ev_pool.size()) {
+      EventPair p{};
+      p.kid = kid;
+      HIPCHK(c, hipEventCreate(&p.a));
+      HIPCHK(c, hipEventCreate(&p.b));
+      c->ev_pool.push_back(p);
+    }
+    ep = &c->ev_pool[c->ev_used++];
+    ep->kid = kid;
+    HIPCHK(c, hipEventRecord(ep->a, c->stream));
+  }
+  fn();
+  HIPCHK(c, hipGetLastError());
+  if (ep) HIPCHK(c, hipEventRecord(ep->b, c->stream));
+  return PFMPE_OK;
+}
+
+int harvest_timing(pfmpe_ctx* c) {
+  for (size_t i = 0; i < c->ev_used; ++i) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_pool[i].a, c->ev_pool[i].b));
+    c->k_launches[c->ev_pool[i].kid] += 1;
+    c->k_ms[c->ev_pool[i].kid] += ms;
+  }
+  c->ev_used = 0;
+  return PFMPE_OK;
+}
+
+#define RET(expr)              \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_ != PFMPE_OK) return r_; \
+  } while (0)
+
+// ---------------------------------------------------------------------- typed launch sequence
+template <typename T, int RNG, int MAXM>
+struct Seq {
+  static int prep(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+    return launch(c, PFMPE_K_PREP, [&] {
+      hipLaunchKernelGGL((k_prep<T>), dim3(1), dim3(kBlock), 0, c->stream, fa, blobs,
+                         (BlobTable<T>*)c->d_table, c->d_ctrl);
+    });
+  }
+  static int iterate(pfmpe_ctx* c, const FrameArgs& fa, int iter) {
+    const T* prior = (const T*)c->d_state[c->prior_idx];
+    RET(launch(c, PFMPE_K_PROPAGATE, [&] {
+      if (c->prune)
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true>), dim3(fa.nblk), dim3(kBlock), 0,
+                           c->stream, fa, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1],
+                           (const BlobTable<T>*)c->d_table, c->d_ctrl, iter);
+      else
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false>), dim3(fa.nblk), dim3(kBlock), 0,
+                           c->stream, fa, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1],
+                           (const BlobTable<T>*)c->d_table, c->d_ctrl, iter);
+    }));
+    return launch(c, PFMPE_K_REDUCE, [&] {
+      hipLaunchKernelGGL((k_iter_reduce<RNG>), dim3(1), dim3(kReduceThreads), 0, c->stream, fa, c->d_ctrl,
+                         c->d_part[0], c->d_part[1], c->d_Eb, c->d_Rin, iter);
+    });
+  }
+  static int finish(pfmpe_ctx* c, const FrameArgs& fa) {
+    const T* prior = (const T*)c->d_state[c->prior_idx];
+    T* post = (T*)c->d_state[1 - c->prior_idx];
+    RET(launch(c, PFMPE_K_RESAMPLE, [&] {
+      hipLaunchKernelGGL((k_resample<T, RNG>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl,
+                         prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_Eb, c->d_Rin,
+                         c->d_cparts, c->record_counts ? c->d_counts : nullptr);
+    }));
+    RET(launch(c, PFMPE_K_FINAL, [&] {
+      hipLaunchKernelGGL((k_final<T, RNG, MAXM>), dim3(1), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, prior,
+                         c->d_cparts, (const BlobTable<T>*)c->d_table, c->d_out);
+    }));
+    HIPCHK(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(OutDev), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PFMPE_OK;
+  }
+  static int step(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+    RET(prep(c, fa, blobs));
+    const int iter_cap = fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter);
+    int iter = 0;
+    RET(iterate(c, fa, iter++));
+    RET(finish(c, fa));
+    // Rare path: the exit rule did not fire on iteration 0.  Later iterations are queued in growing
+    // batches; kernels of iterations past the exit are no-ops (they read ctrl->done).
+    int batch = 1;
+    while (!c->h_out->done) {
+      if (iter >= iter_cap) return fail(c, PFMPE_E_STATE, "PF iteration loop did not terminate");
+      for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, iter++));
+      RET(finish(c, fa));
+      batch = std::min(batch * 2, 16);
+    }
+    return PFMPE_OK;
+  }
+  static int regen(pfmpe_ctx* c, const FrameArgs& fa, const void* prior, double* out) {
+    return launch(c, PFMPE_K_FINAL, [&] {
+      hipLaunchKernelGGL((k_regen<T, RNG>), dim3((fa.N + 255) / 256), dim3(256), 0, c->stream, fa, c->d_ctrl,
+                         (const T*)prior, out);
+    });
+  }
+};
+
+template <typename T, int RNG>
+int dispatch_m(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+  if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, blobs);
+  return Seq<T, RNG, 16>::step(c, fa, blobs);
+}
+
+int dispatch_step(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+  const bool f64 = c->state_dtype == PFMPE_STATE_F64;
+  const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
+  if (f64) return ref ? dispatch_m<double, kRngReference>(c, fa, blobs) : dispatch_m<double, kRngPhilox>(c, fa, blobs);
+  return ref ? dispatch_m<float, kRngReference>(c, fa, blobs) : dispatch_m<float, kRngPhilox>(c, fa, blobs);
+}
+
+int dispatch_regen(pfmpe_ctx* c, const FrameArgs& fa, const void* prior, double* out) {
+  const bool f64 = c->state_dtype == PFMPE_STATE_F64;
+  const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
+  if (f64) return ref ? Seq<double, kRngReference, 8>::regen(c, fa, prior, out)
+                      : Seq<double, kRngPhilox, 8>::regen(c, fa, prior, out);
+  return ref ? Seq<float, kRngReference, 8>::regen(c, fa, prior, out)
+             : Seq<float, kRngPhilox, 8>::regen(c, fa, prior, out);
+}
+
+bool is_identity12(const double* p) {
+  static const double I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
+  for (int q = 0; q < 12; ++q)
+    if (p[q] != I[q]) return false;
+  return true;
+}
+
+// FrameArgs from the host state + frame inputs (PE:488-531)
+FrameArgs build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
+  FrameArgs fa{};
+  std::memcpy(fa.cur, in->current_pose, sizeof(fa.cur));
+  std::memcpy(fa.pred, in->predicted_pose, sizeof(fa.pred));
+  std::memcpy(fa.predm, in->prediction, sizeof(fa.predm));
+  std::memcpy(fa.cam, in->cam_move_inv, sizeof(fa.cam));
+  std::memcpy(fa.markers, c->markers, sizeof(fa.markers));
+  std::memcpy(fa.K, c->K, sizeof(fa.K));
+  const pfmpe_params& p = c->params;
+  double facT, facR;
+  if (in->it_since_init == 1) {  // PE:488-496
+    facT = 1;
+    facR = 1;
+  } else {                       // PE:499-505 (all three use predictionMatrix(0,3))
+    facT = std::min(std::max(0.2, std::abs(in->prediction[3]) / in->dt), 1.0) / 4;
+    facR = 0.2;
+  }
+  for (int q = 0; q < 3; ++q) {
+    fa.lo[q] = p.ang_min * facR;
+    fa.hi[q] = p.ang_max * facR;
+    fa.lo[3 + q] = p.trans_min * facT;
+    fa.hi[3 + q] = p.trans_max * facT;
+  }
+  fa.growth = p.growth;
+  fa.tol = p.tol;
+  fa.tol_pf = p.tol_pf;
+  const int B = in->B;
+  fa.exit_thr = (double)((size_t)c->M * (size_t)std::min(p.exit_cap, B));
+  fa.accept_thr = (double)((size_t)c->M * (size_t)std::min(p.accept_cap, B));
+  fa.key0 = (uint32_t)in->seed;
+  fa.key1 = (uint32_t)(in->seed >> 32);
+  fa.flo = (uint32_t)in->frame_idx;
+  fa.fhi = (uint32_t)(in->frame_idx >> 32);
+  fa.lcg_x0 = lcg_seed((uint32_t)in->seed);
+  fa.downgrade = c->downgrade;
+  fa.N = c->N;
+  fa.M = c->M;
+  fa.B = B;
+  fa.it = in->it_since_init;
+  fa.cam_identity = is_identity12(in->cam_move_inv) ? 1 : 0;
+  fa.max_iter = p.max_iter;
+  fa.force_iters = in->force_iters;
+  fa.nblk = (c->N + kBlock - 1) / kBlock;
+  fa.ld = c->ld;
+  return fa;
+}
+
+void free_all(pfmpe_ctx* c) {
+  void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
+                 c->d_Eb, c->d_Rin, c->d_cparts, c->d_table, c->d_ctrl, c->d_out, c->d_blobs,
+                 c->d_bank, c->d_xfer, c->d_counts};
+  for (void* p : dev)
+    if (p) (void)hipFree(p);
+  if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_blobs) (void)hipHostFree(c->h_blobs);
+  for (auto& e : c->ev_pool) {
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
+  }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+}  // namespace
+
+// ======================================================================================= C-ABI
+extern "C" {
+
+int pfmpe_abi_version(void) { return PFMPE_ABI_VERSION; }
+
+void pfmpe_default_params(pfmpe_params* p) {
+  if (!p) return;
+  // README.md:338-361 launch defaults; constants of PE:563, 616, 633
+  p->tol = 5.0;
+  p->tol_pf = 4.0;
+  p->ang_min = -0.015;
+  p->ang_max = 0.015;
+  p->trans_min = -0.035;
+  p->trans_max = 0.035;
+  p->growth = 0.025;
+  p->max_iter = 80;
+  p->exit_cap = 5;
+  p->accept_cap = 3;
+  p->rng_mode = PFMPE_RNG_PHILOX;
+}
+
+int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_markers, int max_blobs,
+                 int state_dtype) {
+  if (!out) return PFMPE_E_ARG;
+  *out = nullptr;
+  if (max_particles < 1 || max_markers < 1 || max_markers > kMaxMarkers || max_blobs < 0 ||
+      max_blobs > kMaxBlobs || (state_dtype != PFMPE_STATE_F32 && state_dtype != PFMPE_STATE_F64))
+    return PFMPE_E_ARG;
+  pfmpe_ctx* c = new pfmpe_ctx();
+  c->device = hip_device;
+  c->max_particles = max_particles;
+  c->max_markers = max_markers;
+  c->max_blobs = max_blobs;
+  c->state_dtype = state_dtype;
+  c->es = state_dtype == PFMPE_STATE_F64 ? 8 : 4;
+  c->ld = ((int64_t)max_particles + 63) / 64 * 64;
+  c->max_blk = (max_particles + kBlock - 1) / kBlock;
+  pfmpe_default_params(&c->params);
+  auto bad = [&](int code) {
+    free_all(c);
+    delete c;
+    return code;
+  };
+  if (hipSetDevice(hip_device) != hipSuccess) return bad(PFMPE_E_HIP);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PFMPE_E_HIP);
+  const size_t state_bytes = (size_t)kPlanes * c->ld * c->es;
+  bool ok = true;
+  for (int i = 0; i < 2; ++i) {
+    ok &= hipMalloc(&c->d_state[i], state_bytes) == hipSuccess;
+    ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->es) == hipSuccess;
+    ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * sizeof(BlockPart)) == hipSuccess;
+  }
+  ok &= hipMalloc((void**)&c->d_Eb, (size_t)c->max_blk * sizeof(double)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_Rin, (size_t)c->max_blk * sizeof(double)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_cparts, (size_t)c->max_blk * sizeof(CountPart)) == hipSuccess;
+  ok &= hipMalloc(&c->d_table, std::max(sizeof(BlobTable<double>), sizeof(BlobTable<float>))) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_out, sizeof(OutDev)) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_out, sizeof(OutDev), hipHostMallocDefault) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_blobs, (size_t)kMaxBlobs * 2 * sizeof(double)) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_blobs, (size_t)kMaxBlobs * 2 * sizeof(double), hipHostMallocDefault) ==
+        hipSuccess;
+  if (!ok) return bad(PFMPE_E_HIP);
+  if (hipMemset(c->d_ctrl, 0, sizeof(Ctrl)) != hipSuccess) return bad(PFMPE_E_HIP);
+  if (hipMemset(c->d_state[0], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
+  if (hipMemset(c->d_state[1], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
+  *out = c;
+  return PFMPE_OK;
+}
+
+void pfmpe_destroy(pfmpe_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  free_all(c);
+  delete c;
+}
+
+const char* pfmpe_last_error(const pfmpe_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int pfmpe_set_model(pfmpe_ctx* c, const double* markers_xyz, int M, const double* K, const uint8_t* downgrade) {
+  if (!c) return PFMPE_E_ARG;
+  if (!markers_xyz || !K || M < 1) return fail(c, PFMPE_E_ARG, "set_model: null markers/K or M < 1");
+  if (M > c->max_markers) return fail(c, PFMPE_E_CAP, "set_model: M exceeds max_markers");
+  c->M = M;
+  std::memset(c->markers, 0, sizeof(c->markers));
+  std::memcpy(c->markers, markers_xyz, sizeof(double) * 3 * M);
+  std::memcpy(c->K, K, sizeof(c->K));
+  c->downgrade = 0;
+  if (downgrade)
+    for (int j = 0; j < M; ++j)
+      if (downgrade[j]) c->downgrade |= 1u << j;
+  c->has_model = true;
+  return PFMPE_OK;
+}
+
+int pfmpe_set_params(pfmpe_ctx* c, const pfmpe_params* p) {
+  if (!c || !p) return PFMPE_E_ARG;
+  if (!(p->tol > 0) || !(p->tol_pf >= 0) || p->max_iter < 1 || p->exit_cap < 0 || p->accept_cap < 0 ||
+      (p->rng_mode != PFMPE_RNG_REFERENCE && p->rng_mode != PFMPE_RNG_PHILOX))
+    return fail(c, PFMPE_E_ARG, "set_params: invalid parameter");
+  c->params = *p;
+  return PFMPE_OK;
+}
+
+int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
+  if (!c) return PFMPE_E_ARG;
+  switch (option) {
+    case PFMPE_OPT_RECORD_COUNTS:
+      c->record_counts = value != 0;
+      if (c->record_counts && !c->d_counts) {
+        RET(set_device(c));
+        HIPCHK(c, hipMalloc((void**)&c->d_counts, (size_t)c->ld * sizeof(uint32_t)));
+      }
+      return PFMPE_OK;
+    case PFMPE_OPT_PRUNE:
+      c->prune = value != 0;
+      return PFMPE_OK;
+    case PFMPE_OPT_TIMING:
+      c->timing = value != 0;
+      return PFMPE_OK;
+    default:
+      return fail(c, PFMPE_E_ARG, "set_option: unknown option");
+  }
+}
+
+static int ensure_xfer(pfmpe_ctx* c) {
+  if (!c->d_xfer) HIPCHK(c, hipMalloc((void**)&c->d_xfer, (size_t)c->max_particles * 12 * sizeof(double)));
+  return PFMPE_OK;
+}
+
+int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
+  if (!c) return PFMPE_E_ARG;
+  if (!poses || N < 1) return fail(c, PFMPE_E_ARG, "set_prior: null poses or N < 1");
+  if (N > c->max_particles) return fail(c, PFMPE_E_CAP, "set_prior: N exceeds max_particles");
+  RET(set_device(c));
+  RET(ensure_xfer(c));
+  HIPCHK(c, hipMemcpyAsync(c->d_xfer, poses, (size_t)N * 12 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (c->state_dtype == PFMPE_STATE_F64)
+    hipLaunchKernelGGL((k_import<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
+                       (double*)c->d_state[c->prior_idx], N, c->ld);
+  else
+    hipLaunchKernelGGL((k_import<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
+                       (float*)c->d_state[c->prior_idx], N, c->ld);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->N = N;
+  c->has_prior = true;
+  c->has_last = false;
+  return PFMPE_OK;
+}
+
+int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offsets, int nframes) {
+  if (!c) return PFMPE_E_ARG;
+  if (!blobs || !offsets || nframes < 1) return fail(c, PFMPE_E_ARG, "stage_blob_bank: bad arguments");
+  for (int f = 0; f < nframes; ++f) {
+    const int B = offsets[f + 1] - offsets[f];
+    if (B < 0 || offsets[f] < 0) return fail(c, PFMPE_E_ARG, "stage_blob_bank: offsets not monotone");
+    if (B > c->max_blobs) return fail(c, PFMPE_E_CAP, "stage_blob_bank: frame exceeds max_blobs");
+  }
+  RET(set_device(c));
+  if (c->d_bank) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->d_bank));
+    c->d_bank = nullptr;
+  }
+  const size_t rows = (size_t)std::max(1, offsets[nframes]);
+  HIPCHK(c, hipMalloc((void**)&c->d_bank, rows * 2 * sizeof(double)));
+  if (offsets[nframes] > 0)
+    HIPCHK(c, hipMemcpy(c->d_bank, blobs, (size_t)offsets[nframes] * 2 * sizeof(double), hipMemcpyHostToDevice));
+  c->bank_off.assign(offsets, offsets + nframes + 1);
+  return PFMPE_OK;
+}
+
+int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!in || !out) return fail(c, PFMPE_E_ARG, "step: null in/out");
+  if (!c->has_model || !c->has_prior) return fail(c, PFMPE_E_STATE, "step: set_model and set_prior first");
+  if (in->B < 0) return fail(c, PFMPE_E_ARG, "step: B < 0");
+  if (in->B > c->max_blobs) return fail(c, PFMPE_E_CAP, "step: B exceeds max_blobs");
+  if (in->it_since_init >= 2 && !(in->dt != 0.0))
+    return fail(c, PFMPE_E_ARG, "step: dt must be non-zero in steady state");
+  RET(set_device(c));
+  const double* blobs = c->d_blobs;
+  int B = in->B;
+  if (in->bank_frame >= 0) {
+    if (!c->d_bank || in->bank_frame + 1 >= (int)c->bank_off.size())
+      return fail(c, PFMPE_E_ARG, "step: bank_frame out of range");
+    const int off = c->bank_off[in->bank_frame];
+    B = c->bank_off[in->bank_frame + 1] - off;
+    if (B != in->B) return fail(c, PFMPE_E_ARG, "step: B does not match the staged bank frame");
+    blobs = c->d_bank + 2 * (size_t)off;
+  } else if (B > 0) {
+    if (!in->blobs) return fail(c, PFMPE_E_ARG, "step: null blobs");
+    std::memcpy(c->h_blobs, in->blobs, (size_t)B * 2 * sizeof(double));
+    HIPCHK(c, hipMemcpyAsync(c->d_blobs, c->h_blobs, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice,
+                             c->stream));
+  }
+  const FrameArgs fa = build_args(c, in);
+  RET(dispatch_step(c, fa, blobs));
+  if (c->timing) RET(harvest_timing(c));
+
+  const OutDev& o = *c->h_out;
+  out->iters = o.iters;
+  out->kept_iter = o.kept_iter;
+  out->most_likely_idx = o.most_likely_idx;
+  out->accepted = o.accepted;
+  out->resampled = o.resampled;
+  out->winner_idx = o.winner_idx;
+  out->n_corr = o.n_corr;
+  out->flag_fail = o.flag_fail;
+  out->highest_prob = o.highest_prob;
+  out->prob_sum = o.prob_sum;
+  std::memcpy(out->winner_pose, o.winner_pose, sizeof(out->winner_pose));
+  std::memcpy(out->most_likely_pose, o.most_likely_pose, sizeof(out->most_likely_pose));
+  std::memcpy(out->corr, o.corr, sizeof(out->corr));
+
+  c->last_fa = fa;
+  c->has_last = true;
+  c->last_prior_idx = c->prior_idx;
+  c->last_accepted = o.resampled != 0;
+  if (o.resampled) c->prior_idx = 1 - c->prior_idx;  // newPoseEstimation = resampled set (PE:681, 727)
+  return PFMPE_OK;
+}
+
+int pfmpe_get_particles(pfmpe_ctx* c, int which, double* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!out || (which != 0 && which != 1)) return fail(c, PFMPE_E_ARG, "get_particles: bad arguments");
+  if (!c->has_prior) return fail(c, PFMPE_E_STATE, "get_particles: no particle set");
+  if (which == 0 && !c->has_last) return fail(c, PFMPE_E_STATE, "get_particles(0): no step yet");
+  RET(set_device(c));
+  RET(ensure_xfer(c));
+  const int N = c->N;
+  if (which == 0) {
+    RET(dispatch_regen(c, c->last_fa, c->d_state[c->last_prior_idx], c->d_xfer));
+  } else if (c->state_dtype == PFMPE_STATE_F64) {
+    hipLaunchKernelGGL((k_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
+                       (const double*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld);
+  } else {
+    hipLaunchKernelGGL((k_export<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
+                       (const float*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld);
+  }
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, c->d_xfer, (size_t)N * 12 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->ev_used = 0;
+  return PFMPE_OK;
+}
+
+int pfmpe_get_weights(pfmpe_ctx* c, double* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!out) return fail(c, PFMPE_E_ARG, "get_weights: null out");
+  if (!c->has_last) return fail(c, PFMPE_E_STATE, "get_weights: no step yet");
+  RET(set_device(c));
+  RET(ensure_xfer(c));
+  const int N = c->N;
+  if (c->state_dtype == PFMPE_STATE_F64)
+    hipLaunchKernelGGL((k_weights_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_ctrl,
+                       (const double*)c->d_w[0], (const double*)c->d_w[1], c->d_xfer, N);
+  else
+    hipLaunchKernelGGL((k_weights_export<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_ctrl,
+                       (const float*)c->d_w[0], (const float*)c->d_w[1], c->d_xfer, N);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, c->d_xfer, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PFMPE_OK;
+}
+
+int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!out) return fail(c, PFMPE_E_ARG, "get_counts: null out");
+  if (!c->record_counts || !c->d_counts) return fail(c, PFMPE_E_STATE, "get_counts: PFMPE_OPT_RECORD_COUNTS off");
+  if (!c->has_last || !c->last_accepted) return fail(c, PFMPE_E_STATE, "get_counts: last step did not resample");
+  RET(set_device(c));
+  HIPCHK(c, hipMemcpy(out, c->d_counts, (size_t)c->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return PFMPE_OK;
+}
+
+int pfmpe_get_kernel_stats(pfmpe_ctx* c, int kernel, int64_t* launches, double* total_ms) {
+  if (!c || kernel < 0 || kernel >= PFMPE_K_COUNT) return PFMPE_E_ARG;
+  if (launches) *launches = c->k_launches[kernel];
+  if (total_ms) *total_ms = c->k_ms[kernel];
+  return PFMPE_OK;
+}
+
+int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
+  if (!c) return PFMPE_E_ARG;
+  for (int k = 0; k < PFMPE_K_COUNT; ++k) {
+    c->k_launches[k] = 0;
+    c->k_ms[k] = 0;
+  }
+  return PFMPE_OK;
+}
+
+const char* pfmpe_kernel_name(int kernel) {
+  static const char* names[PFMPE_K_COUNT] = {"k_prep", "k_propagate_weigh", "k_iter_reduce", "k_resample",
+                                             "k_final"};
+  return (kernel >= 0 && kernel < PFMPE_K_COUNT) ? names[kernel] : "?";
+}
+
+// ---- host-side evaluation of the device RNG code (CPU tests pin it against the oracle)
+double pfmpe_host_ref_uniform(uint32_t seed, uint64_t j, double a, double b) {
+  const uint32_t x0 = lcg_seed(seed);
+  const uint32_t g1 = lcg_output(x0, 2 * j + 1);
+  const uint32_t g2 = lcg_next(g1);
+  return ref_uniform(ref_canonical(g1, g2), a, b);
+}
+
+void pfmpe_host_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  const U32x4 o = philox4x32_10(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]);
+  out[0] = o.x;
+  out[1] = o.y;
+  out[2] = o.z;
+  out[3] = o.w;
+}
+
+}  // extern "C"

@@ -1,0 +1,323 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle on identical inputs.
+
+Bars (SURVEY.md §7 "minimum slice", north_star):
+  * fp64 state (PFMPE_STATE_F64), either RNG stream: every discrete output identical to the oracle
+    (iterations, kept iteration, accept, most-likely index, resample counts, winner, correspondences);
+    weights within 1e-9 absolute, poses within 1e-9 (ulp-level differences only: sin/cos libraries).
+  * fp32 state (the throughput path): weights within 2e-3 absolute for >= 99.5 % of particles (a marker
+    sitting within ~1e-5 px of the tol_PF gate may flip), accept decision identical, counts sum to N,
+    winner/pose tolerance 1e-4 m / 1e-3 rad against the oracle's winner pose where the winners agree.
+"""
+import numpy as np
+import pytest
+
+import pf_monocular_pose_estimator_amd as pf
+from pf_monocular_pose_estimator_amd import synthetic as syn
+from oracle import pforacle as orc
+
+pytestmark = pytest.mark.gpu
+
+RNG = {"ref": pf.RNG_REFERENCE, "philox": pf.RNG_PHILOX}
+STATE = {"f64": pf.STATE_F64, "f32": pf.STATE_F32}
+
+
+def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None):
+    eng = pf.Engine(device=0, max_particles=max(N, 1), state_dtype=state)
+    eng.set_model(markers, K, downgrade)
+    prm = params or pf.default_params()
+    prm.rng_mode = rng
+    eng.set_params(prm)
+    eng.set_option(pf.OPT_RECORD_COUNTS, 1)
+    eng.set_option(pf.OPT_PRUNE, 1 if prune else 0)
+    return eng
+
+
+def orc_params_from(prm):
+    return orc.OrcParams(prm.tol, prm.tol_pf, prm.ang_min, prm.ang_max, prm.trans_min, prm.trans_max, prm.growth,
+                         prm.max_iter, prm.exit_cap, prm.accept_cap, prm.rng_mode)
+
+
+def step_both(eng, prm, markers, K, prior, cur, pred, predm, blobs, seed, frame_idx, it=2, dt=0.02,
+              force_iters=0, cam=None, downgrade=None):
+    fr = eng.make_frame(cur, pred, predm, blobs=blobs, dt=dt, seed=seed, frame_idx=frame_idx, it_since_init=it,
+                        force_iters=force_iters, cam_move_inv=cam)
+    out = eng.step(fr).as_dict()
+    gpu = {"weights": eng.get_weights(), "propagated": eng.get_particles(0)}
+    if out["resampled"]:
+        gpu["counts"] = eng.get_counts()
+        gpu["resampled"] = eng.get_particles(1)
+    ref, arr = orc.pf_step(markers, K, orc_params_from(prm), prior, cur, pred, predm, blobs, it_since_init=it, dt=dt,
+                           seed=seed, frame_idx=frame_idx, force_iters=force_iters, cam_move_inv=cam,
+                           downgrade=downgrade)
+    return out, gpu, ref, arr
+
+
+def assert_exact(out, gpu, ref, arr, N):
+    for k in ("iters", "kept_iter", "accepted", "resampled", "most_likely_idx", "winner_idx", "n_corr", "flag_fail"):
+        assert out[k] == ref[k], (k, out[k], ref[k])
+    assert np.array_equal(out["pairs"], ref["pairs"])
+    np.testing.assert_allclose(gpu["weights"], arr["weights"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(gpu["propagated"], arr["propagated"], rtol=0, atol=1e-9)
+    assert out["highest_prob"] == pytest.approx(ref["highest_prob"], abs=1e-9)
+    assert out["prob_sum"] == pytest.approx(ref["prob_sum"], rel=1e-12, abs=1e-9)
+    np.testing.assert_allclose(out["winner_pose"], ref["winner_pose"], rtol=0, atol=1e-9)
+    np.testing.assert_allclose(out["most_likely_pose"], ref["most_likely_pose"], rtol=0, atol=1e-9)
+    if out["resampled"]:
+        assert np.array_equal(gpu["counts"], arr["counts"])
+        assert int(gpu["counts"].sum()) <= N
+        np.testing.assert_allclose(gpu["resampled"], arr["resampled"], rtol=0, atol=1e-9)
+
+
+CASES = [  # (N, M, B, heavy)
+    (1000, 5, 20, False),
+    (4099, 5, 50, False),
+    (2048, 12, 200, True),
+]
+
+
+@pytest.mark.parametrize("rng", ["ref", "philox"])
+@pytest.mark.parametrize("N,M,B,heavy", CASES)
+@pytest.mark.parametrize("prune", [True, False])
+def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune):
+    cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
+    st = syn.make_stream(cfg, 3)
+    prm = pf.default_params()
+    prm.rng_mode = RNG[rng]
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng], prune=prune)
+    prior = st.prior()
+    eng.set_prior(prior)
+    for fr in st.frames:
+        out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior, fr.current_pose, fr.predicted_pose,
+                                       fr.prediction, fr.blobs, seed=1000 + fr.index, frame_idx=fr.index)
+        assert_exact(out, gpu, ref, arr, N)
+        if out["resampled"]:
+            prior = arr["resampled"]
+    eng.close()
+
+
+@pytest.mark.parametrize("rng", ["ref", "philox"])
+def test_fp64_exit_rule_runs_all_iterations(rng):
+    """One LED occluded -> max weight < M*min(5,B): the loop runs all 80 iterations with noise growth
+    and keeps the earliest strictly-best iteration (PE:606-624)."""
+    N = 96
+    cfg = syn.StreamConfig("t", M=5, B=12, N=N)
+    st = syn.make_stream(cfg, 1)
+    fr = st.frames[0]
+    true_px = syn.project(st.K, fr.truth, st.markers)
+    blobs = np.vstack([true_px[1:], fr.blobs[:7]]).astype(np.float32).astype(np.float64)
+    prm = pf.default_params()
+    prm.rng_mode = RNG[rng]
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng])
+    prior = st.prior()
+    eng.set_prior(prior)
+    out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior, fr.current_pose, fr.predicted_pose,
+                                   fr.prediction, blobs, seed=77, frame_idx=3)
+    assert ref["iters"] == 80
+    assert_exact(out, gpu, ref, arr, N)
+    eng.close()
+
+
+@pytest.mark.parametrize("state", ["f64", "f32"])
+@pytest.mark.parametrize("N", [1, 2, 3, 257])
+def test_small_particle_counts(state, N):
+    cfg = syn.StreamConfig("t", M=5, B=20, N=N)
+    st = syn.make_stream(cfg, 2)
+    prm = pf.default_params()
+    prm.rng_mode = pf.RNG_REFERENCE
+    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_REFERENCE)
+    prior = st.prior()
+    eng.set_prior(prior)
+    for fr in st.frames:
+        prior_used = eng.get_particles(1)
+        out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior_used, fr.current_pose, fr.predicted_pose,
+                                       fr.prediction, fr.blobs, seed=5 + fr.index, frame_idx=fr.index)
+        if state == "f64":
+            assert_exact(out, gpu, ref, arr, N)
+        else:
+            assert out["accepted"] == ref["accepted"]
+            np.testing.assert_allclose(gpu["weights"], arr["weights"], atol=2e-3)
+    eng.close()
+
+
+@pytest.mark.parametrize("state", ["f64", "f32"])
+def test_no_blobs_reinitialises(state):
+    N = 300
+    cfg = syn.StreamConfig("t", M=5, B=20, N=N)
+    st = syn.make_stream(cfg, 1)
+    fr = st.frames[0]
+    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX)
+    prm = pf.default_params()
+    eng.set_prior(st.prior())
+    for blobs in (np.zeros((0, 2)), np.array([[5000.0, 5000.0], [6000.0, -40.0]])):
+        out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, st.prior(), fr.current_pose, fr.predicted_pose,
+                                       fr.prediction, blobs, seed=9, frame_idx=1)
+        assert out["accepted"] == 0 and ref["accepted"] == 0
+        assert out["flag_fail"] == pf.FLAG_REINIT
+        assert out["iters"] == ref["iters"] == 80
+        assert out["most_likely_idx"] == ref["most_likely_idx"]
+        assert out["winner_idx"] == -1
+    eng.close()
+
+
+def test_fp64_fewer_blobs_than_markers_and_downgrade_and_cam_motion():
+    N = 512
+    cfg = syn.StreamConfig("t", M=5, B=3, N=N)
+    st = syn.make_stream(cfg, 1)
+    fr = st.frames[0]
+    dg = np.array([1, 0, 0, 1, 0], np.uint8)
+    cam = syn.to12(syn.se3_exp([0.002, -0.001, 0.003, 0.001, 0.0005, -0.002]))
+    prm = pf.default_params()
+    prm.rng_mode = pf.RNG_REFERENCE
+    prm.accept_cap = 2
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, pf.RNG_REFERENCE, downgrade=dg, params=prm)
+    prior = st.prior()
+    eng.set_prior(prior)
+    true_px = syn.project(st.K, fr.truth, st.markers)
+    blobs = true_px[[0, 2, 4]].astype(np.float32).astype(np.float64)
+    for it, force in ((2, 0), (1, 4), (2, 13)):
+        out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior, fr.current_pose, fr.predicted_pose,
+                                       fr.prediction, blobs, seed=31 + it, frame_idx=2, it=it, force_iters=force,
+                                       cam=cam, downgrade=dg)
+        assert_exact(out, gpu, ref, arr, N)
+        if force:
+            assert out["iters"] == force
+        eng.set_prior(prior)
+    eng.close()
+
+
+def _collapsed_scenario():
+    """Hand-built prior with both strongly positive and NEGATIVE weights (self-occlusion penalties),
+    to exercise the running-max semantics of the cumulative search (SURVEY.md §7 hard part 3)."""
+    K = syn.K_README
+    s = 0.02
+    markers = np.array([[-s, -s, 0.0], [s, -s, 0.0], [s, s, 0.0], [-s, s, 0.0]])
+    T_true = np.eye(4)
+    T_true[:3, 3] = [0.0, 0.0, 2.0]
+    T_far = np.eye(4)
+    T_far[:3, 3] = [0.0, 0.0, 40.0]
+    px_true = syn.project(K, T_true, markers)
+    centre = syn.project(K, T_far, markers).mean(axis=0) + np.array([3.4, 0.0])
+    blobs = np.vstack([px_true, centre[None]])
+    N = 64
+    poses = []
+    for n in range(N):
+        poses.append(syn.to12(T_true if n % 3 else T_far))
+    return K, markers, np.array(poses), blobs, syn.to12(T_true)
+
+
+@pytest.mark.parametrize("rng", ["ref", "philox"])
+def test_fp64_negative_weights_running_max(rng):
+    K, markers, prior, blobs, truth = _collapsed_scenario()
+    N = prior.shape[0]
+    prm = pf.default_params()
+    prm.rng_mode = RNG[rng]
+    prm.ang_min = prm.ang_max = prm.trans_min = prm.trans_max = 0.0
+    eng = make_engine(N, markers, K, pf.STATE_F64, RNG[rng], params=prm)
+    eng.set_prior(prior)
+    ident = np.eye(4)[:3].reshape(12)
+    out, gpu, ref, arr = step_both(eng, prm, markers, K, prior, truth, truth, ident, blobs, seed=3, frame_idx=0, it=1)
+    assert (arr["weights"] < 0).any() and (arr["weights"] > 15).any()
+    assert out["accepted"] == 1
+    assert_exact(out, gpu, ref, arr, N)
+    eng.close()
+
+
+@pytest.mark.parametrize("rng", ["ref", "philox"])
+@pytest.mark.parametrize("N,M,B,heavy", [(20000, 5, 50, False), (8192, 12, 200, True)])
+def test_fp32_tolerance(rng, N, M, B, heavy):
+    cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
+    st = syn.make_stream(cfg, 3)
+    prm = pf.default_params()
+    prm.rng_mode = RNG[rng]
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F32, RNG[rng])
+    eng.set_prior(st.prior())
+    for fr in st.frames:
+        prior_used = eng.get_particles(1)  # float-representable values: the oracle starts from the same set
+        out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior_used, fr.current_pose, fr.predicted_pose,
+                                       fr.prediction, fr.blobs, seed=50 + fr.index, frame_idx=fr.index)
+        assert out["accepted"] == ref["accepted"]
+        assert out["iters"] == ref["iters"]
+        dw = np.abs(gpu["weights"] - arr["weights"])
+        assert np.mean(dw <= 2e-3) >= 0.995, np.sort(dw)[-10:]
+        dp = np.abs(gpu["propagated"] - arr["propagated"])
+        assert dp[:, [0, 1, 2, 4, 5, 6, 8, 9, 10]].max() < 1e-5 and dp[:, [3, 7, 11]].max() < 1e-5
+        if out["resampled"]:
+            c = gpu["counts"].astype(np.int64)
+            assert c.sum() <= N and (c >= 0).all()
+            same = np.mean(c == arr["counts"])
+            assert same >= 0.97, same
+            # the winner has the maximum count (first on ties) and its pose is the propagated particle
+            w = out["winner_idx"]
+            assert c[w] == c.max() and np.argmax(c) == w
+            np.testing.assert_allclose(out["winner_pose"], gpu["propagated"][w], atol=1e-6)
+            # correspondences of the winner equal the oracle likelihood evaluated on that pose
+            proj = np.array([orc.project(st.K, gpu["propagated"][w], X) for X in st.markers])
+            _, pairs = orc.likelihood(proj, fr.blobs, prm.tol, prm.tol_pf)
+            assert np.array_equal(out["pairs"], pairs)
+    eng.close()
+
+
+@pytest.mark.parametrize("N", [1_000_000])
+def test_fp32_large_n_properties(N):
+    """BASELINE-size property checks (the O(N^2) oracle cannot run at 1M): counts sum to N, every new
+    prior particle is a copy of a propagated particle, weights of a random subset match the oracle
+    likelihood evaluated in fp64 on the GPU's own propagated poses."""
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 1)
+    fr = st.frames[0]
+    prm = pf.default_params()
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F32, pf.RNG_PHILOX)
+    eng.set_prior(st.prior())
+    out = eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt,
+                                  seed=4, frame_idx=0))
+    assert out.accepted == 1
+    w = eng.get_weights()
+    prop = eng.get_particles(0)
+    counts = eng.get_counts().astype(np.int64)
+    post = eng.get_particles(1)
+    assert counts.sum() == N  # every target finds a particle in practice (normalised total == 1)
+    owner = np.repeat(np.arange(N), counts)
+    np.testing.assert_array_equal(post, prop[owner])
+    rng = np.random.default_rng(0)
+    sub = rng.choice(N, 1500, replace=False)
+    bad = 0
+    for n in sub:
+        proj = np.array([orc.project(st.K, prop[n], X) for X in st.markers])
+        P, _ = orc.likelihood(proj, fr.blobs, prm.tol, prm.tol_pf)
+        bad += abs(P - w[n]) > 2e-3
+    assert bad <= 3
+    assert out.winner_idx == int(np.argmax(counts))
+    eng.close()
+
+
+def test_blob_bank_matches_host_blobs():
+    N = 5000
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 3)
+    a = make_engine(N, st.markers, st.K, pf.STATE_F32, pf.RNG_PHILOX)
+    b = make_engine(N, st.markers, st.K, pf.STATE_F32, pf.RNG_PHILOX)
+    a.set_prior(st.prior())
+    b.set_prior(st.prior())
+    b.stage_blob_bank([f.blobs for f in st.frames])
+    for fr in st.frames:
+        oa = a.step(a.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt,
+                                 seed=8, frame_idx=fr.index)).as_dict()
+        ob = b.step(b.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, B=len(fr.blobs),
+                                 bank_frame=fr.index, dt=fr.dt, seed=8, frame_idx=fr.index)).as_dict()
+        for k in ("iters", "winner_idx", "accepted", "highest_prob", "prob_sum"):
+            assert oa[k] == ob[k]
+        np.testing.assert_array_equal(a.get_particles(1), b.get_particles(1))
+    a.close()
+    b.close()
+
+
+def test_api_errors_on_gpu():
+    eng = pf.Engine(device=0, max_particles=100, state_dtype=pf.STATE_F32)
+    with pytest.raises(pf.PFError):
+        eng.step(eng.make_frame(np.eye(4)[:3], np.eye(4)[:3], np.eye(4)[:3], blobs=np.zeros((1, 2))))
+    eng.set_model(syn.MARKERS_5, syn.K_README)
+    with pytest.raises(pf.PFError):
+        eng.set_prior(np.zeros((101, 12)))
+    with pytest.raises(pf.PFError):
+        eng.set_model(np.zeros((17, 3)), syn.K_README)
+    eng.close()
