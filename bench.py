@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    ap.add_argument("--diag", type=int, default=0, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -53,7 +54,7 @@ def algorithmic_bytes(S: int, N: int) -> dict:
     return {
         "k_propagate_weigh": N * (S + 4),      # read prior state, write weight
         "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
-        "k_iter_reduce": 0, "k_prep": 0, "k_final": 0,
+        "aux": 0,
     }
 
 
@@ -103,6 +104,8 @@ def main():
     prm.rng_mode = pf.RNG_PHILOX if args.rng == "philox" else pf.RNG_REFERENCE
     eng.set_params(prm)
     eng.set_prior(st.prior())
+    if args.diag:
+        eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])
     frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
                              dt=f.dt, seed=(rank << 32) + 17 + f.index, frame_idx=f.index,

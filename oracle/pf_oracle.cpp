@@ -236,10 +236,10 @@ inline void philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], ui
 }
 
 // Counter layout shared with the HIP engine (DESIGN.md "RNG"):
-//   motion   ctr = {n, iter | tag<<24, frame_lo, frame_hi}, tag 0 -> (a,b,c,tx), tag 1 -> (ty,tz)
-//   resample ctr = {k, 2<<24,           frame_lo, frame_hi}
+//   motion   ctr = {n, iter | 0<<24, frame_lo, frame_hi} -> six 21-bit uniforms (a,b,c,tx,ty,tz)
+//   resample ctr = {k, 2<<24,        frame_lo, frame_hi} -> one 53-bit uniform
 //   key      = {seed_lo, seed_hi}
-inline double u24(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }
+inline double u21(uint32_t v) { return (double)v * (1.0 / 2097152.0); }
 inline double u53(uint32_t x0, uint32_t x1) {
   return ((double)(x0 >> 5) * 67108864.0 + (double)(x1 >> 6)) * (1.0 / 9007199254740992.0);
 }
@@ -421,12 +421,12 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
           dr[1] = randAngleY(generator);
           dr[2] = randAngleZ(generator);
         } else {
-          uint32_t ca[4] = {(uint32_t)n, (uint32_t)iter | (0u << 24), flo, fhi}, oa[4];
-          uint32_t cb[4] = {(uint32_t)n, (uint32_t)iter | (1u << 24), flo, fhi}, ob[4];
-          philox4x32_10(ca, key, oa);
-          philox4x32_10(cb, key, ob);
-          const double u[6] = {u24(oa[0]), u24(oa[1]), u24(oa[2]), u24(oa[3]), u24(ob[0]), u24(ob[1])};
-          for (int q = 0; q < 6; ++q) dr[q] = u[q] * (hi[q] - lo[q]) + lo[q];
+          // one Philox call -> six 21-bit uniforms (top 21 bits of each word, then two from the low bits)
+          uint32_t ca[4] = {(uint32_t)n, (uint32_t)iter | (0u << 24), flo, fhi}, o[4];
+          philox4x32_10(ca, key, o);
+          const uint32_t v[6] = {o[0] >> 11, o[1] >> 11, o[2] >> 11, o[3] >> 11,
+                                 ((o[0] & 0x7FFu) << 10) | (o[1] & 0x3FFu), ((o[2] & 0x7FFu) << 10) | (o[3] & 0x3FFu)};
+          for (int q = 0; q < 6; ++q) dr[q] = u21(v[q]) * (hi[q] - lo[q]) + lo[q];
         }
         const double a = dr[0] * g;
         const double b = dr[1] * g;
@@ -543,6 +543,44 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
   }
   to12(PoseParticle[out->most_likely_idx], out->most_likely_pose);
   if (counts_out) std::copy(counterMeas.begin(), counterMeas.end(), counts_out);
+  return 0;
+}
+
+// Stratified resampling alone (PE:627-682) on given raw weights: normalise (sequential fp64 sum), draw
+// U_k from the stream position the PF block leaves it at (reference mode: after 12*(N-2)*iters engine
+// outputs; Philox: resample counters), first-i cumulative search.  Used to check the GPU resampler on
+// the GPU's own fp32 weights.  Returns 0 if resampled, 1 if the sum is zero.
+int orc_stratified_resample(int N, const double* raw_weights, int rng_mode, uint64_t seed, uint64_t frame_idx,
+                            int iters, unsigned* counts_out, int* idx_out) {
+  std::vector<double> w(raw_weights, raw_weights + N);
+  double S = 0;
+  for (int n = 0; n < N; ++n) S += w[n];
+  std::fill(counts_out, counts_out + N, 0u);
+  if (S == 0) return 1;
+  for (int n = 0; n < N; ++n) w[n] = w[n] / S;
+  std::default_random_engine generator((uint32_t)seed);
+  if (rng_mode == RNG_REFERENCE && N > 2) generator.discard((unsigned long long)12 * (N - 2) * (unsigned long long)iters);
+  const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  const uint32_t flo = (uint32_t)frame_idx, fhi = (uint32_t)(frame_idx >> 32);
+  int Particle_index = N - 1;
+  for (int k = 0; k < N; ++k) {
+    double u;
+    if (rng_mode == RNG_REFERENCE) {
+      std::uniform_real_distribution<double> randResample(0, 1);
+      u = randResample(generator);
+    } else {
+      uint32_t cr[4] = {(uint32_t)k, 2u << 24, flo, fhi}, o[4];
+      philox4x32_10(cr, key, o);
+      u = u53(o[0], o[1]);
+    }
+    const double randVar = (k + u) / N;
+    double c = 0;
+    for (int i = 0; i < N; ++i) {
+      c += w[i];
+      if (c >= randVar) { Particle_index = i; counts_out[i]++; break; }
+    }
+    if (idx_out) idx_out[k] = Particle_index;
+  }
   return 0;
 }
 

@@ -88,6 +88,9 @@ def load() -> C.CDLL:
     lib.orc_pf_step.restype = C.c_int
     lib.orc_pf_step.argtypes = [C.c_int, C.c_int, dp, dp, u8p, C.POINTER(OrcParams), C.POINTER(OrcFrameIn), dp,
                                 C.POINTER(OrcFrameOut), dp, dp, dp, C.POINTER(C.c_int), up]
+    lib.orc_stratified_resample.restype = C.c_int
+    lib.orc_stratified_resample.argtypes = [C.c_int, dp, C.c_int, C.c_uint64, C.c_uint64, C.c_int, up,
+                                            C.POINTER(C.c_int)]
     lib.orc_exp_map.restype = None
     lib.orc_exp_map.argtypes = [dp, dp]
     lib.orc_log_map.restype = None
@@ -202,6 +205,17 @@ def pf_step(markers, K, params: OrcParams, prior, current_pose, predicted_pose, 
     if rc != 0:
         raise RuntimeError(f"orc_pf_step failed: {rc}")
     return out.as_dict(), arrays
+
+
+def stratified_resample(weights, rng_mode, seed, frame_idx, iters):
+    """PE:627-682 alone on the given raw weights -> (counts, idx)."""
+    w = _d(weights)
+    N = w.size
+    counts = np.zeros(N, dtype=np.uint32)
+    idx = np.zeros(N, dtype=np.int32)
+    load().orc_stratified_resample(N, _p(w), rng_mode, seed, frame_idx, iters,
+                                   counts.ctypes.data_as(C.POINTER(C.c_uint)), idx.ctypes.data_as(C.POINTER(C.c_int)))
+    return counts, idx
 
 
 def exp_map(twist):

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64 = 0, 1
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING = 1, 2, 3
-K_PREP, K_PROPAGATE, K_REDUCE, K_RESAMPLE, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_COUNT = 0, 1, 2, 3
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (

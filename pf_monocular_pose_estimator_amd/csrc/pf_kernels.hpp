@@ -1,20 +1,31 @@
 // pf_kernels.hpp — HIP kernels of the PF step for gfx950 (MI355X, CDNA4, wave64).
 //
-// One frame (reference PE:475-733) runs as:
-//   k_prep            1 block : blob table (blobs sorted by x + x-bucket index) + control reset
-//   k_propagate_weigh nblk    : per particle: motion model (PE:543-588) -> project M markers (PE:1017)
-//                               -> likelihood (PE:2385) -> weight; per-block partials
-//                               (sum / running-sum extrema / max / min of the weights)
-//   k_iter_reduce     1 block : iteration max, best-iteration bookkeeping and exit rule (PE:606-616);
-//                               on the last iteration: normaliser S, block prefixes, accept (PE:627-633)
-//   (k_propagate_weigh, k_iter_reduce) repeat only if the exit rule is not met (rare in steady state)
-//   k_resample        nblk    : stratified resampling (PE:666-682) as a parallel scan + target count
-//                               + wave-cooperative scatter of regenerated particles into the new prior
-//   k_final           1 block : winner = argmax resample count (PE:685-688), its pose + pairs
+// One frame (reference PE:475-733) is two launches:
+//
+//   k_propagate_weigh  one particle per thread.  Per block: an x-bucketed blob table in LDS; per
+//                      particle the motion model (PE:543-588) -> projection of M markers (PE:1017) ->
+//                      likelihood (PE:2385) -> weight.  Per-block partials are handed (write-through,
+//                      counter) to the last block of each 64-block GROUP, whose wave scans the group;
+//                      group partials go to the last group, whose wave does the iteration bookkeeping
+//                      and exit rule (PE:606-616) and, on the final iteration, the normaliser S, the
+//                      group prefixes and the accept test (PE:627-633).  Re-launched only if the exit
+//                      rule did not fire (rare in steady state).
+//   k_resample         stratified resampling (PE:666-682) as a parallel scan + target count per
+//                      particle + wave-cooperative scatter of regenerated particles into the new prior.
+//                      Count partials go up the same 2-level tree; the last group's wave picks the
+//                      winner = argmax count (PE:685-688), computes its pose and pairs and writes the
+//                      frame record straight into pinned host memory.
 //
 // Propagated particles are never written to HBM: they are regenerated from (prior[n], RNG counter)
-// where needed (resample scatter, winner), so the HBM traffic per particle-update is the compulsory
-// 3*S + 8 bytes (S = 48 B for fp32 SoA state; DESIGN.md "Roofline").
+// where needed, so the HBM traffic per particle-update is the compulsory 3*S + 8 bytes (S = 48 B for
+// fp32 SoA state; DESIGN.md "Roofline").
+//
+// Normalised cumulative weight (DESIGN.md "Exact tiling of the stratified targets"): for particle i of
+// block b in group g,   c_i = fl( fl( G_g + fl( E_b + incl_i ) ) / S )
+// with incl_i the in-block prefix, E_b the in-group exclusive prefix and G_g the group prefix.  For a
+// fixed (g, S) c_i is monotone in fl(E_b + incl_i), so every running maximum the resampler needs at a
+// block boundary is composed EXACTLY (max has no rounding) from group-local max-scans: the slot ranges
+// of all particles tile [0, N) with no gap and no overlap.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <float.h>
@@ -27,72 +38,79 @@ namespace pfmpe {
 
 constexpr int kBlock = 256;            // particles per block (4 waves)
 constexpr int kWaves = kBlock / 64;
+constexpr int kGroup = 64;             // blocks per reduction group (one per lane of the group wave)
 constexpr int kMaxMarkers = 16;
 constexpr int kMaxBlobs = 1024;
 constexpr int kBuckets = 128;          // x-buckets of the blob table
-constexpr int kReduceThreads = 1024;   // single-block reducer
 constexpr int kPlanes = 12;            // r00 r01 r02 t0 r10 r11 r12 t1 r20 r21 r22 t2
 
 enum : int { kRngReference = 0, kRngPhilox = 1 };
 
 // ----------------------------------------------------------------------------- kernel arguments
-// Passed by value (kernarg segment -> scalar loads).  Doubles are converted to T on use.
-struct FrameArgs {
-  double cur[12], pred[12], predm[12], cam[12];  // 3x4 row-major
-  double markers[kMaxMarkers * 3];
-  double K[9];
-  double lo[6], hi[6];      // draw ranges: angX angY angZ tX tY tZ (already scaled by fac*)
+// Passed by value (kernarg segment -> scalar loads), pre-converted to the compute type T on the host.
+template <typename T>
+struct FrameArgsT {
+  T cur[12], pred[12], predm[12], cam[12];  // 3x4 row-major
+  T markers[kMaxMarkers * 3];
+  T K[9];
+  T lo[6], hi[6];           // draw ranges angX angY angZ tX tY tZ (scaled by fac*), Philox stream
+  double dlo[6], dhi[6];    // the same in double, reference stream (draws are computed in double)
   double growth;            // 0.025
-  double tol, tol_pf;       // score normaliser / acceptance gate
+  T tol, tol_pf, tolq;      // score normaliser / acceptance gate / pruning half-window
   double exit_thr, accept_thr;
   uint32_t key0, key1, flo, fhi;  // philox key / frame counter
   uint32_t lcg_x0;                // reference engine state after seeding
   uint32_t downgrade;             // bit j: marker j downgraded
   int32_t N, M, B, it;            // particles, markers, blobs, it_since_initialized_
   int32_t cam_identity, max_iter, force_iters, nblk;
+  int32_t ngrp, diag;             // groups; diagnostic switches (0 in production)
   int64_t ld;                     // SoA plane stride in elements
 };
 
+// Per-frame control record.  All-zero is the valid "start of frame" state (zeroed at create, set_prior
+// and by the final wave of every frame).
 struct Ctrl {
   double best_max;   // highestProb
   double S;          // probPartSum of the kept iteration
-  double Rmax;       // max running cumulative normalised weight
+  double Rmax;       // max normalised cumulative weight (running max at the last particle)
   int32_t done, has_best, best_idx, best_iter, best_slot, cur_slot;
   int32_t iters, kept_slot, kept_iter, accepted, most_likely_idx, pad0;
   int64_t K_total;   // number of stratified targets that find a particle
 };
 
-struct BlockPart {   // per propagate block, per weight slot
-  double sum;        // sum of weights (fp64)
-  double maxrel;     // max / min of the in-block inclusive prefix sums
-  double minrel;
-  double maxw, minw; // max / min weight
+// per block, per weight slot (written and read write-through)
+struct alignas(16) BlockPart {
+  double sum;             // block total (in-block scan order)
+  double maxrel, minrel;  // extrema of the in-block inclusive prefix sums
+  double maxw, minw;      // max / min weight
   int32_t argmax, argmin;
 };
-
-struct CountPart {
+// per group, per weight slot (write-through)
+struct alignas(16) GroupPart {
+  double sum;          // group total
+  double zmax, zmin;   // max / min over the group of fl(E_b + incl_i)
+  double maxw, minw;
+  int32_t argmax, argmin;
+};
+// per block, per weight slot: in-group exclusive prefix E_b and exclusive max/min of z (for k_resample)
+struct alignas(16) BlockScan {
+  double E, zin_max, zin_min, pad;
+};
+// per group, kept slot only: group prefix G_g and running max of c at the group start
+struct alignas(16) GroupScan {
+  double G, Gin;
+};
+struct alignas(8) CountPart {
   int32_t maxcount, idx;
 };
 
-// device copy of the frame output (pfmpe_frame_out layout + done word)
+// frame record written by the final wave into pinned host memory (pfmpe_frame_out layout + 2 words)
 struct OutDev {
-  int32_t done, pad;
+  int32_t done, kept_slot;
   int32_t iters, kept_iter, most_likely_idx, accepted, resampled, winner_idx, n_corr, flag_fail;
   double highest_prob, prob_sum;
   double winner_pose[12], most_likely_pose[12];
   uint32_t corr[2 * kMaxMarkers];
-};
-
-// blob table (written by k_prep, read into LDS by the propagate kernel)
-template <typename T>
-struct BlobTable {
-  T bx[kMaxBlobs];       // sorted by (x, original index)
-  T by[kMaxBlobs];
-  int32_t orig[kMaxBlobs];
-  int32_t bstart[kBuckets + 1];
-  T xmin, inv_bw, b0x, b0y;  // bucket origin / inverse width, original blob 0
-  T tolq;                    // conservative search half-width (>= tol_pf)
-  int32_t B;
 };
 
 // ----------------------------------------------------------------------------- scalar helpers
@@ -100,7 +118,18 @@ __device__ __forceinline__ float fmadd(float a, float b, float c) { return __bui
 // fp64: deliberately UNFUSED (TU built with -ffp-contract=off): a*b rounded, then +c rounded, the
 // reference's x86-64 arithmetic.
 __device__ __forceinline__ double fmadd(double a, double b, double c) { return a * b + c; }
-__device__ __forceinline__ void sincos_t(float x, float* s, float* c) { sincosf(x, s, c); }
+// fp32: the motion noise angles are tiny (|x| <= 0.015 * 1.x rad with README parameters), so a short
+// Taylor polynomial is accurate to float rounding there; larger angles take sincosf.
+__device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
+  if (fabsf(x) <= 0.25f) {
+    const float x2 = x * x;
+    *s = x * fmadd(x2, fmadd(x2, fmadd(x2, fmadd(x2, 1.0f / 362880.0f, -1.0f / 5040.0f), 1.0f / 120.0f),
+                             -1.0f / 6.0f), 1.0f);
+    *c = fmadd(x2, fmadd(x2, fmadd(x2, fmadd(x2, 1.0f / 40320.0f, -1.0f / 720.0f), 1.0f / 24.0f), -0.5f), 1.0f);
+  } else {
+    sincosf(x, s, c);
+  }
+}
 __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
   *s = sin(x);
   *c = cos(x);
@@ -140,22 +169,18 @@ __device__ __forceinline__ void compose(const T* A, const T* B, T* C) {
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void load12(const double* src, T* dst) {
-#pragma unroll
-  for (int q = 0; q < 12; ++q) dst[q] = (T)src[q];
-}
-
 // The motion model (PE:543-588) for particle n in PF iteration `iter`; P receives the 3x4 pose.
 template <typename T, int RNG>
-__device__ __forceinline__ void make_particle(const FrameArgs& fa, const T* __restrict__ prior, int n,
+__device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const T* __restrict__ prior, int n,
                                               int iter, T* P) {
   if (n == 0) {  // current_pose_ (PE:547)
-    load12(fa.cur, P);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) P[q] = fa.cur[q];
     return;
   }
   if (n == 1) {  // predicted_pose_ (PE:551)
-    load12(fa.pred, P);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) P[q] = fa.pred[q];
     return;
   }
   T A[12];
@@ -163,16 +188,14 @@ __device__ __forceinline__ void make_particle(const FrameArgs& fa, const T* __re
   for (int q = 0; q < 12; ++q) A[q] = prior[(int64_t)q * fa.ld + n];
   if (fa.it > 1) {
     if (!fa.cam_identity) {  // camMoveInv * prior (PE:556-558)
-      T C[12], X[12];
-      load12(fa.cam, C);
-      compose(C, A, X);
+      T X[12];
+      compose(fa.cam, A, X);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = X[q];
     }
     if ((iter % 10) != 0) {  // ... * predictionMatrix (PE:556)
-      T Pm[12], X[12];
-      load12(fa.predm, Pm);
-      compose(A, Pm, X);
+      T X[12];
+      compose(A, fa.predm, X);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = X[q];
     }
@@ -181,29 +204,22 @@ __device__ __forceinline__ void make_particle(const FrameArgs& fa, const T* __re
   const double gd = 1.0 + fa.growth * (double)(iter / 10);
   T d[6];
   if (RNG == kRngReference) {
-    const uint64_t per_particle = 12u;
-    const uint64_t before = per_particle * ((uint64_t)(fa.N - 2) * (uint64_t)iter + (uint64_t)(n - 2));
+    const uint64_t before = 12u * ((uint64_t)(fa.N - 2) * (uint64_t)iter + (uint64_t)(n - 2));
     uint32_t g = lcg_output(fa.lcg_x0, before + 1u);
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const uint32_t g1 = g;
       const uint32_t g2 = lcg_next(g1);
       g = lcg_next(g2);
-      const double u = ref_canonical(g1, g2);
-      d[q] = (T)(ref_uniform(u, fa.lo[q], fa.hi[q]) * gd);
+      d[q] = (T)(ref_uniform(ref_canonical(g1, g2), fa.dlo[q], fa.dhi[q]) * gd);
     }
   } else {
-    const U32x4 ra = philox4x32_10((uint32_t)n, (uint32_t)iter | (kTagMotionA << 24), fa.flo, fa.fhi,
-                                   fa.key0, fa.key1);
-    const U32x4 rb = philox4x32_10((uint32_t)n, (uint32_t)iter | (kTagMotionB << 24), fa.flo, fa.fhi,
-                                   fa.key0, fa.key1);
-    const uint32_t raw[6] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y};
+    const Draws6 r = philox_motion6((uint32_t)n, (uint32_t)iter, fa.flo, fa.fhi, fa.key0, fa.key1);
     const T g = (T)gd;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-      const T lo = (T)fa.lo[q], hi = (T)fa.hi[q];
-      const T u = (T)u24d(raw[q]);
-      const T draw = u * (hi - lo) + lo;
+      const T u = (T)u21d(r.v[q]);
+      const T draw = u * (fa.hi[q] - fa.lo[q]) + fa.lo[q];
       d[q] = draw * g;
     }
   }
@@ -230,23 +246,22 @@ __device__ __forceinline__ void make_particle(const FrameArgs& fa, const T* __re
 
 // project2d (PE:1017-1034): p = (K34*T) * [X;1], u = p/p.z — full K, no distortion, no z>0 test
 template <typename T, int MAXM>
-__device__ __forceinline__ void project_markers(const FrameArgs& fa, const T* P, T* u, T* v) {
+__device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const T* P, T* u, T* v) {
   T Q[12];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const T k0 = (T)fa.K[i * 3 + 0], k1 = (T)fa.K[i * 3 + 1], k2 = (T)fa.K[i * 3 + 2];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      T s = k0 * P[0 * 4 + j];
-      s = fmadd(k1, P[1 * 4 + j], s);
-      s = fmadd(k2, P[2 * 4 + j], s);
+      T s = fa.K[i * 3 + 0] * P[0 * 4 + j];
+      s = fmadd(fa.K[i * 3 + 1], P[1 * 4 + j], s);
+      s = fmadd(fa.K[i * 3 + 2], P[2 * 4 + j], s);
       Q[i * 4 + j] = s;
     }
   }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     if (j < fa.M) {
-      const T X = (T)fa.markers[3 * j], Y = (T)fa.markers[3 * j + 1], Z = (T)fa.markers[3 * j + 2];
+      const T X = fa.markers[3 * j], Y = fa.markers[3 * j + 1], Z = fa.markers[3 * j + 2];
       T p[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -271,26 +286,21 @@ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
   return (int)f;
 }
 
-// calculateEstimationProbability (PE:2385-2445) in its closed form: per marker the first-minimum blob
-// (exact; candidates limited to the conservative x-window that contains every blob within tol_PF, so
-// pruning never changes an accepted pair — DESIGN.md "Exact blob pruning"), then extraction in
-// ascending (distance, marker) order = the order Eigen's minCoeff visits, with the same gate, score
-// (tol, not tol_PF), self-occlusion and downgrade penalties.
-template <typename T, int MAXM, bool PRUNE, bool PAIRS>
-__device__ __forceinline__ T likelihood(const FrameArgs& fa, const T* u, const T* v, const T* bx,
-                                        const T* by, const int32_t* orig, const int32_t* bstart,
-                                        T xmin, T inv_bw, T b0x, T b0y, T tolq, uint32_t* pairs,
-                                        int* npairs) {
+// calculateEstimationProbability (PE:2385-2445) in its closed form.  Step 1: per marker the first-minimum
+// blob over all blobs (column minimum of the B x M distance matrix; ties -> lowest blob index).
+// Step 2 (score_minima): extraction in ascending (distance, marker) order — the order Eigen's minCoeff
+// visitor finds them — with the same gate (tol_PF), score ((tol-d)/tol)^2 with tol NOT tol_PF,
+// self-occlusion (3*s) and downgrade (2) penalties, capped at min(B, M) pairs.
+//
+// Exact pruning (DESIGN.md "Exact blob pruning"): only blobs inside the x-window |bx-u| <= tolq
+// (tolq >= tol_PF plus rounding slack) are visited.  Every blob within tol_PF lies in the window, and a
+// marker whose true minimum lies outside it fails the gate anyway, so accepted pairs, penalties and the
+// weight are unchanged; rejected markers only change their (unused) distance value.
+template <typename T, int MAXM, bool PRUNE>
+__device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* u, const T* v, const T* bx,
+                                              const T* by, const int32_t* orig, const int32_t* bstart,
+                                              T xmin, T inv_bw, T* m, int* r) {
   const int B = fa.B, M = fa.M;
-  if (PAIRS) *npairs = 0;
-  if (B == 0) return (T)0;
-  {  // Eigen's visitor starts from coeff(0,0): a NaN there poisons the first minCoeff -> break
-    const T dx = b0x - u[0], dy = b0y - v[0];
-    const T d = dx * dx + dy * dy;
-    if (d != d) return (T)0;
-  }
-  T m[MAXM];
-  int r[MAXM];
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     T best = inf_t<T>();
@@ -298,8 +308,8 @@ __device__ __forceinline__ T likelihood(const FrameArgs& fa, const T* u, const T
     if (j < M) {
       int c0 = 0, c1 = B;
       if (PRUNE) {
-        c0 = bstart[bucket_of(u[j] - tolq, xmin, inv_bw)];
-        c1 = bstart[bucket_of(u[j] + tolq, xmin, inv_bw) + 1];
+        c0 = bstart[bucket_of(u[j] - fa.tolq, xmin, inv_bw)];
+        c1 = bstart[bucket_of(u[j] + fa.tolq, xmin, inv_bw) + 1];
       }
       for (int c = c0; c < c1; ++c) {
         const T dx = bx[c] - u[j];
@@ -315,11 +325,26 @@ __device__ __forceinline__ T likelihood(const FrameArgs& fa, const T* u, const T
     m[j] = best;
     r[j] = (arg == 0x7fffffff) ? 0 : arg;
   }
+}
+
+// Eigen's visitor starts from coeff(0,0): a NaN distance there poisons the first minCoeff -> break at k=0
+template <typename T>
+__device__ __forceinline__ bool nan_at_origin(T b0x, T b0y, T u0, T v0) {
+  const T dx = b0x - u0, dy = b0y - v0;
+  const T d = dx * dx + dy * dy;
+  return d != d;
+}
+
+template <typename T, int MAXM, bool PAIRS>
+__device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, const int* r, uint32_t* pairs,
+                                          int* npairs) {
+  const int B = fa.B, M = fa.M;
   const int L = B < M ? B : M;
-  const T tol = (T)fa.tol, tol_pf = (T)fa.tol_pf, Mt = (T)M;
+  const T tol = fa.tol, tol_pf = fa.tol_pf, Mt = (T)M;
   T Pr = (T)0;
   int s = 1;
   uint32_t taken = 0u;
+  if (PAIRS) *npairs = 0;
   for (int k = 0; k < L; ++k) {
     T best = (T)0;
     int jb = -1, rb = 0;
@@ -376,49 +401,84 @@ __device__ __forceinline__ double wave_incl_max(double v) {
   }
   return v;
 }
+__device__ __forceinline__ double wave_incl_min(double v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double t = __shfl_up(v, off, 64);
+    if (lane >= off && t < v) v = t;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double t = __shfl_xor(v, off, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double t = __shfl_xor(v, off, 64);
+    v = t < v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_incl_sum_int(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(v, off, 64);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
 // (value, index): larger value wins, lower index on ties
-__device__ __forceinline__ void cmb_max(double& v, int& i, double v2, int i2) {
+template <typename V>
+__device__ __forceinline__ void cmb_max(V& v, int& i, V v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) {
     v = v2;
     i = i2;
   }
 }
-__device__ __forceinline__ void cmb_min(double& v, int& i, double v2, int i2) {
+template <typename V>
+__device__ __forceinline__ void cmb_min(V& v, int& i, V v2, int i2) {
   if (v2 < v || (v2 == v && i2 < i)) {
     v = v2;
     i = i2;
   }
 }
-__device__ __forceinline__ void wave_argmax(double& v, int& i) {
+template <typename V>
+__device__ __forceinline__ void wave_argmax(V& v, int& i) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cmb_max(v, i, __shfl_xor(v, off, 64), __shfl_xor(i, off, 64));
+  for (int off = 32; off > 0; off >>= 1) cmb_max(v, i, (V)__shfl_xor(v, off, 64), (int)__shfl_xor(i, off, 64));
 }
-__device__ __forceinline__ void wave_argmin(double& v, int& i) {
+template <typename V>
+__device__ __forceinline__ void wave_argmin(V& v, int& i) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cmb_min(v, i, __shfl_xor(v, off, 64), __shfl_xor(i, off, 64));
+  for (int off = 32; off > 0; off >>= 1) cmb_min(v, i, (V)__shfl_xor(v, off, 64), (int)__shfl_xor(i, off, 64));
 }
 
-// Deterministic block inclusive scan (same code in the propagate and resample kernels, so both see
-// bit-identical prefix sums).  sh: >= kWaves doubles.
-__device__ __forceinline__ void block_incl_sum(double v, double& incl, double& total, double* sh) {
+// Deterministic block inclusive scan: pre_w = ((0 + t_0) + t_1) + ... over earlier waves' totals, then
+// incl = pre_w + (wave inclusive).  k_propagate_weigh derives its partial extrema with exactly this
+// association, so both launches see bit-identical prefixes.  sh: >= kWaves doubles.
+__device__ __forceinline__ void block_incl_sum(double v, double& incl, double* sh) {
   const double wi = wave_incl_sum(v);
   if (lane_id() == 63) sh[wave_id()] = wi;
   __syncthreads();
-  double pre = 0.0, tot = 0.0;
+  double pre = 0.0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) {
+  for (int w = 0; w < kWaves; ++w)
     if (w < wave_id()) pre = pre + sh[w];
-    tot = tot + sh[w];
-  }
   incl = pre + wi;
-  total = tot;
-  __syncthreads();
 }
 
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
-template <int RNG>
-__device__ __forceinline__ double target_r(const FrameArgs& fa, int iters, int64_t k) {
+template <typename T, int RNG>
+__device__ __forceinline__ double target_r(const FrameArgsT<T>& fa, int iters, int64_t k) {
   double U;
   if (RNG == kRngReference) {
     const uint64_t motion = fa.N > 2 ? (uint64_t)12 * (uint64_t)(fa.N - 2) * (uint64_t)iters : 0u;
@@ -435,50 +495,127 @@ __device__ __forceinline__ double target_r(const FrameArgs& fa, int iters, int64
 // F(x) = #{k : r_k <= x}.  r_k is non-decreasing in k, so target k finds the first particle i whose
 // running-max cumulative weight R_i >= r_k (reference: first i with cumsum_i >= r_k, PE:674-679),
 // and particle i receives F(R_i) - F(R_{i-1}) copies.
-template <int RNG>
-__device__ __forceinline__ int64_t count_targets(const FrameArgs& fa, int iters, double x) {
+template <typename T, int RNG>
+__device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int iters, double x) {
   const int64_t N = fa.N;
   if (!(x >= 0.0)) return 0;  // r_k >= 0; also -inf / NaN
   const double fk = floor(x * (double)N);
   int64_t k = fk < 0.0 ? 0 : (fk > (double)N ? N : (int64_t)fk);
-  while (k < N && target_r<RNG>(fa, iters, k) <= x) ++k;
-  while (k > 0 && target_r<RNG>(fa, iters, k - 1) > x) --k;
+  while (k < N && target_r<T, RNG>(fa, iters, k) <= x) ++k;
+  while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
   return k;
 }
 
+// ----------------------------------------------------------------------------- in-launch hand-off
+// Per-block / per-group partials go to the last arriver (MI355X_MICROARCH.md "Valid forms", row 1):
+// every partial word is stored write-through (sc1, agent scope) by the one lane that then drains
+// (s_waitcnt vmcnt(0)) and adds to ONE unsharded counter; the arriver whose add returns count-1 is
+// last and its wave reads the partials with sc1 loads.  No buffer_wbl2 / buffer_inv fences: those
+// write back the XCD's whole dirty L2 (the weights / new prior this kernel streams) once per block.
+typedef __attribute__((address_space(1))) uint64_t gu64_t;
+typedef __attribute__((address_space(1))) uint32_t gu32_t;
+
+__device__ __forceinline__ void st_wt(void* p, uint64_t v) {
+  __hip_atomic_store((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt_d(double* p, double v) { st_wt(p, (uint64_t)__double_as_longlong(v)); }
+__device__ __forceinline__ uint64_t ld_wt(const void* p) {
+  return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt_d(const double* p) { return __longlong_as_double((long long)ld_wt(p)); }
+__device__ __forceinline__ uint64_t pack2(int a, int b) { return (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32); }
+__device__ __forceinline__ int lo32(uint64_t v) { return (int)(uint32_t)v; }
+__device__ __forceinline__ int hi32(uint64_t v) { return (int)(uint32_t)(v >> 32); }
+
+// one lane, after its sc1 partial stores; returns true for the last of `count` arrivers
+__device__ __forceinline__ bool arrive_last(uint32_t* counter, int count) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const uint32_t prev = __hip_atomic_fetch_add((gu32_t*)counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool last = prev == (uint32_t)(count - 1);
+  if (last) __hip_atomic_store((gu32_t*)counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  return last;
+}
+// wave-uniform "am I last" decided by lane 0
+__device__ __forceinline__ bool wave_arrive_last(uint32_t* counter, int count) {
+  int last = 0;
+  if (lane_id() == 0) last = arrive_last(counter, count) ? 1 : 0;
+  return __shfl(last, 0, 64) != 0;
+}
+
+// Diagnostic stamps (fa.diag & 4 only): s_memrealtime (100 MHz)
+__device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_min(uint64_t* st, int idx, uint64_t t) {
+  if (st) atomicMin((unsigned long long*)(st + idx), (unsigned long long)t);
+}
+__device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
+  if (st) atomicMax((unsigned long long*)(st + idx), (unsigned long long)t);
+}
+
 // ============================================================================== kernels
-// ---- per-frame preparation: blob table + control reset (1 block)
+// ---- per-block blob table in LDS (dynamic shared memory, sized by B): blobs grouped into x-buckets by a
+// counting sort.  Within a bucket the order is whatever the LDS atomics produce: candidate minima use
+// the explicit (distance, original index) order, so no result depends on it.
 template <typename T>
-__global__ __launch_bounds__(kBlock) void k_prep(const FrameArgs fa, const double* __restrict__ blobs,
-                                                 BlobTable<T>* __restrict__ tab, Ctrl* __restrict__ ctrl) {
-  __shared__ T sx[kMaxBlobs];
-  __shared__ T sy[kMaxBlobs];
-  __shared__ T sred[2 * kWaves];
-  const int B = fa.B;
+struct LdsBlobs {
+  T* bx;
+  T* by;
+  int32_t* orig;
+  int32_t* bstart;  // kBuckets + 1
+  int32_t* fill;    // kBuckets
+  T xmin, inv_bw, b0x, b0y;
+};
+
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+template <typename T>
+__host__ __device__ constexpr size_t blob_lds_bytes(int B) {
+  return align16((size_t)B * sizeof(T)) * 2 + align16((size_t)B * 4) + align16((kBuckets + 1) * 4) +
+         align16(kBuckets * 4) + align16(2 * kWaves * sizeof(T));
+}
+
+template <typename T>
+__device__ LdsBlobs<T> build_blob_table(const FrameArgsT<T>& fa, const double* __restrict__ blobs,
+                                        unsigned char* smem) {
+  const int B = fa.B, tid = threadIdx.x;
+  LdsBlobs<T> t;
+  size_t off = 0;
+  t.bx = (T*)(smem + off);
+  off += align16((size_t)B * sizeof(T));
+  t.by = (T*)(smem + off);
+  off += align16((size_t)B * sizeof(T));
+  t.orig = (int32_t*)(smem + off);
+  off += align16((size_t)B * 4);
+  t.bstart = (int32_t*)(smem + off);
+  off += align16((kBuckets + 1) * 4);
+  t.fill = (int32_t*)(smem + off);
+  off += align16(kBuckets * 4);
+  T* red = (T*)(smem + off);
+
   T lmin = inf_t<T>(), lmax = -inf_t<T>();
-  for (int i = threadIdx.x; i < B; i += kBlock) {
-    const T x = (T)blobs[2 * i], y = (T)blobs[2 * i + 1];
-    sx[i] = x;
-    sy[i] = y;
+  for (int i = tid; i < B; i += kBlock) {
+    const T x = (T)blobs[2 * i];
     lmin = x < lmin ? x : lmin;
     lmax = x > lmax ? x : lmax;
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const T a = __shfl_xor(lmin, off, 64), b = __shfl_xor(lmax, off, 64);
+  for (int o = 32; o > 0; o >>= 1) {
+    const T a = __shfl_xor(lmin, o, 64), b = __shfl_xor(lmax, o, 64);
     lmin = a < lmin ? a : lmin;
     lmax = b > lmax ? b : lmax;
   }
   if (lane_id() == 0) {
-    sred[wave_id()] = lmin;
-    sred[kWaves + wave_id()] = lmax;
+    red[wave_id()] = lmin;
+    red[kWaves + wave_id()] = lmax;
+  }
+  for (int b = tid; b < kBuckets; b += kBlock) {
+    t.bstart[b] = 0;
+    t.fill[b] = 0;
   }
   __syncthreads();
-  T xmin = sred[0], xmax = sred[kWaves];
+  T xmin = red[0], xmax = red[kWaves];
 #pragma unroll
   for (int w = 1; w < kWaves; ++w) {
-    xmin = sred[w] < xmin ? sred[w] : xmin;
-    xmax = sred[kWaves + w] > xmax ? sred[kWaves + w] : xmax;
+    xmin = red[w] < xmin ? red[w] : xmin;
+    xmax = red[kWaves + w] > xmax ? red[kWaves + w] : xmax;
   }
   if (B == 0 || !(xmax - xmin < inf_t<T>())) {
     xmin = (T)0;
@@ -487,274 +624,167 @@ __global__ __launch_bounds__(kBlock) void k_prep(const FrameArgs fa, const doubl
   T span = xmax - xmin;
   if (!(span > (T)0)) span = (T)1;
   const T inv_bw = (T)kBuckets / span;
-  // stable rank sort by (x, index)
-  for (int i = threadIdx.x; i < B; i += kBlock) {
-    const T x = sx[i];
-    int rank = 0;
-    for (int j = 0; j < B; ++j) {
-      const T xj = sx[j];
-      rank += (xj < x || (xj == x && j < i)) ? 1 : 0;
-    }
-    tab->bx[rank] = x;
-    tab->by[rank] = sy[i];
-    tab->orig[rank] = i;
+  for (int i = tid; i < B; i += kBlock) atomicAdd(&t.bstart[bucket_of((T)blobs[2 * i], xmin, inv_bw)], 1);
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 128 bucket counts, two per lane
+    const int c0 = t.bstart[2 * tid], c1 = t.bstart[2 * tid + 1];
+    const int incl = wave_incl_sum_int(c0 + c1);
+    const int excl = incl - c0 - c1;
+    t.bstart[2 * tid] = excl;
+    t.bstart[2 * tid + 1] = excl + c0;
+    if (tid == 63) t.bstart[kBuckets] = incl;
   }
-  // bstart[b] = #{i : bucket(x_i) < b}
-  for (int b = threadIdx.x; b <= kBuckets; b += kBlock) {
-    int c = 0;
-    for (int i = 0; i < B; ++i) c += bucket_of(sx[i], xmin, inv_bw) < b ? 1 : 0;
-    tab->bstart[b] = c;
+  __syncthreads();
+  for (int i = tid; i < B; i += kBlock) {
+    const T x = (T)blobs[2 * i], y = (T)blobs[2 * i + 1];
+    const int b = bucket_of(x, xmin, inv_bw);
+    const int pos = t.bstart[b] + atomicAdd(&t.fill[b], 1);
+    t.bx[pos] = x;
+    t.by[pos] = y;
+    t.orig[pos] = i;
   }
-  if (threadIdx.x == 0) {
-    tab->xmin = xmin;
-    tab->inv_bw = inv_bw;
-    tab->b0x = B > 0 ? sx[0] : (T)0;
-    tab->b0y = B > 0 ? sy[0] : (T)0;
-    // conservative window half-width: every blob with sqrt(d2) <= tol_pf in T arithmetic has
-    // |dx| <= tolq (relative + absolute slack covers rounding of dx*dx+dy*dy and sqrt)
-    tab->tolq = (T)(fa.tol_pf * (1.0 + 1e-3) + 1e-3);
-    tab->B = B;
-    Ctrl c;
-    c.best_max = 0.0;
-    c.S = 0.0;
-    c.Rmax = -INFINITY;
-    c.done = 0;
-    c.has_best = 0;
-    c.best_idx = 0;
-    c.best_iter = 0;
-    c.best_slot = 0;
-    c.cur_slot = 0;
-    c.iters = 0;
-    c.kept_slot = 0;
-    c.kept_iter = 0;
-    c.accepted = 0;
-    c.most_likely_idx = 0;
-    c.pad0 = 0;
-    c.K_total = 0;
-    *ctrl = c;
+  t.xmin = xmin;
+  t.inv_bw = inv_bw;
+  t.b0x = B > 0 ? (T)blobs[0] : (T)0;
+  t.b0y = B > 0 ? (T)blobs[1] : (T)0;
+  __syncthreads();
+  return t;
+}
+
+// ---- group wave of k_propagate_weigh: lanes <-> the <= 64 blocks of group g
+__device__ void propagate_group(int nblk, int g, const BlockPart* __restrict__ part, BlockScan* __restrict__ bscan,
+                                GroupPart* __restrict__ gpart) {
+  const int lane = lane_id();
+  const int b = g * kGroup + lane;
+  const bool vb = b < nblk;
+  double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY, maxw = -INFINITY, minw = INFINITY;
+  int amax = 0x7fffffff, amin = 0x7fffffff;
+  if (vb) {
+    const BlockPart* p = part + b;
+    sum = ld_wt_d(&p->sum);
+    maxrel = ld_wt_d(&p->maxrel);
+    minrel = ld_wt_d(&p->minrel);
+    maxw = ld_wt_d(&p->maxw);
+    minw = ld_wt_d(&p->minw);
+    const uint64_t ai = ld_wt(&p->argmax);
+    amax = lo32(ai);
+    amin = hi32(ai);
+  }
+  const double incl = wave_incl_sum(sum);
+  const double prev = __shfl_up(incl, 1, 64);
+  const double E = lane == 0 ? 0.0 : prev;  // exclusive prefix = previous lane's inclusive value
+  const double zmax = vb ? E + maxrel : -INFINITY;
+  const double zmin = vb ? E + minrel : INFINITY;
+  const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
+  const double zp_max = __shfl_up(zi_max, 1, 64), zp_min = __shfl_up(zi_min, 1, 64);
+  if (vb) {
+    BlockScan s;
+    s.E = E;
+    s.zin_max = lane == 0 ? -INFINITY : zp_max;
+    s.zin_min = lane == 0 ? INFINITY : zp_min;
+    s.pad = 0.0;
+    bscan[b] = s;
+  }
+  const double gsum = __shfl(incl, 63, 64);
+  const double gzmax = __shfl(zi_max, 63, 64), gzmin = __shfl(zi_min, 63, 64);
+  wave_argmax(maxw, amax);
+  wave_argmin(minw, amin);
+  if (lane == 0) {
+    GroupPart* gp = gpart + g;
+    st_wt_d(&gp->sum, gsum);
+    st_wt_d(&gp->zmax, gzmax);
+    st_wt_d(&gp->zmin, gzmin);
+    st_wt_d(&gp->maxw, maxw);
+    st_wt_d(&gp->minw, minw);
+    st_wt(&gp->argmax, pack2(amax, amin));
   }
 }
 
-// ---- motion + projection + likelihood, one particle per thread
-template <typename T, int RNG, int MAXM, bool PRUNE>
-__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
-    const FrameArgs fa, const T* __restrict__ prior, T* __restrict__ w0, T* __restrict__ w1,
-    BlockPart* __restrict__ p0, BlockPart* __restrict__ p1, const BlobTable<T>* __restrict__ tab,
-    const Ctrl* __restrict__ ctrl, int iter) {
-  __shared__ T s_bx[kMaxBlobs];
-  __shared__ T s_by[kMaxBlobs];
-  __shared__ int32_t s_orig[kMaxBlobs];
-  __shared__ int32_t s_bstart[kBuckets + 1];
-  __shared__ double s_sum[kWaves];
-  __shared__ double s_ext[4 * kWaves];
-  __shared__ int s_idx[2 * kWaves];
-
-  if (ctrl->done) return;  // the exit rule already fired (uniform)
-  const int slot = ctrl->cur_slot;
-  const int B = fa.B;
-  for (int i = threadIdx.x; i < B; i += kBlock) {
-    s_bx[i] = tab->bx[i];
-    s_by[i] = tab->by[i];
-    s_orig[i] = tab->orig[i];
-  }
-  for (int b = threadIdx.x; b <= kBuckets; b += kBlock) s_bstart[b] = tab->bstart[b];
-  const T xmin = tab->xmin, inv_bw = tab->inv_bw, b0x = tab->b0x, b0y = tab->b0y, tolq = tab->tolq;
-  __syncthreads();
-
-  const int n = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = n < fa.N;
-  T w = (T)0;
-  if (valid) {
-    T P[12], u[MAXM], v[MAXM];
-    make_particle<T, RNG>(fa, prior, n, iter, P);
-    project_markers<T, MAXM>(fa, P, u, v);
-    w = likelihood<T, MAXM, PRUNE, false>(fa, u, v, s_bx, s_by, s_orig, s_bstart, xmin, inv_bw, b0x,
-                                          b0y, tolq, nullptr, nullptr);
-    (slot ? w1 : w0)[n] = w;
-  }
-  // per-block partials: sum, running-sum extrema, max/argmax, min/argmin
-  const double wd = valid ? (double)w : 0.0;
-  double incl, tot;
-  block_incl_sum(wd, incl, tot, s_sum);
-  double mx = valid ? wd : -INFINITY, mn = valid ? wd : INFINITY;
-  int ix = valid ? n : 0x7fffffff, in_ = ix;
-  double rmax = valid ? incl : -INFINITY, rmin = valid ? incl : INFINITY;
-  wave_argmax(mx, ix);
-  wave_argmin(mn, in_);
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double a = __shfl_xor(rmax, off, 64), b = __shfl_xor(rmin, off, 64);
-    rmax = a > rmax ? a : rmax;
-    rmin = b < rmin ? b : rmin;
-  }
-  if (lane_id() == 0) {
-    s_ext[wave_id()] = mx;
-    s_ext[kWaves + wave_id()] = mn;
-    s_ext[2 * kWaves + wave_id()] = rmax;
-    s_ext[3 * kWaves + wave_id()] = rmin;
-    s_idx[wave_id()] = ix;
-    s_idx[kWaves + wave_id()] = in_;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double bmx = s_ext[0], bmn = s_ext[kWaves], brx = s_ext[2 * kWaves], brn = s_ext[3 * kWaves];
-    int bix = s_idx[0], bin = s_idx[kWaves];
-#pragma unroll
-    for (int ww = 1; ww < kWaves; ++ww) {
-      cmb_max(bmx, bix, s_ext[ww], s_idx[ww]);
-      cmb_min(bmn, bin, s_ext[kWaves + ww], s_idx[kWaves + ww]);
-      brx = s_ext[2 * kWaves + ww] > brx ? s_ext[2 * kWaves + ww] : brx;
-      brn = s_ext[3 * kWaves + ww] < brn ? s_ext[3 * kWaves + ww] : brn;
-    }
-    BlockPart bp;
-    bp.sum = tot;
-    bp.maxrel = brx;
-    bp.minrel = brn;
-    bp.maxw = bmx;
-    bp.minw = bmn;
-    bp.argmax = bix;
-    bp.argmin = bin;
-    (slot ? p1 : p0)[blockIdx.x] = bp;
-  }
-}
-
-// ---- iteration bookkeeping + (on the last iteration) normaliser, prefixes, accept (1 block)
-template <int RNG>
-__global__ __launch_bounds__(kReduceThreads) void k_iter_reduce(const FrameArgs fa, Ctrl* __restrict__ ctrl,
-                                                                const BlockPart* __restrict__ p0,
-                                                                const BlockPart* __restrict__ p1,
-                                                                double* __restrict__ Eb,
-                                                                double* __restrict__ Rin, int iter) {
-  constexpr int W = kReduceThreads / 64;
-  __shared__ double sv[W], sv2[W];
-  __shared__ int si[W], si2[W];
-  __shared__ int s_flag[3];
-  __shared__ double s_S;
-
-  if (ctrl->done) return;
-  const int nblk = fa.nblk;
-  const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-  const int chunk = (nblk + kReduceThreads - 1) / kReduceThreads;
-  const int b0 = tid * chunk, b1 = min(nblk, b0 + chunk);
-
-  {  // this iteration's max / first argmax
-    const int slot = ctrl->cur_slot;
-    const BlockPart* P = slot ? p1 : p0;
-    double mv = -INFINITY;
-    int mi = 0x7fffffff;
-    for (int b = b0; b < b1; ++b) cmb_max(mv, mi, P[b].maxw, P[b].argmax);
-    wave_argmax(mv, mi);
-    if (lane == 0) {
-      sv[wv] = mv;
-      si[wv] = mi;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < W; ++w) cmb_max(mv, mi, sv[w], si[w]);
-      Ctrl c = *ctrl;
-      if (mv > c.best_max) {  // strict: PE:608
-        c.best_max = mv;
-        c.best_idx = mi;
-        c.best_iter = iter;
-        c.best_slot = slot;
-        c.has_best = 1;
-      }
-      c.iters = iter + 1;
-      const bool go_on = fa.force_iters > 0 ? (c.iters < fa.force_iters)
-                                            : (c.iters < fa.max_iter && mv < fa.exit_thr);  // PE:616
-      c.done = go_on ? 0 : 1;
-      c.cur_slot = c.has_best ? 1 - c.best_slot : 1 - slot;
-      if (c.done) {
-        c.kept_slot = c.has_best ? c.best_slot : slot;
-        c.kept_iter = c.has_best ? c.best_iter : iter;
-      }
-      *ctrl = c;
-      s_flag[0] = c.done;
-      s_flag[1] = c.kept_slot;
-    }
-    __syncthreads();
-  }
-  if (!s_flag[0]) return;
-  const BlockPart* KP = s_flag[1] ? p1 : p0;
-
-  // exclusive scan of block sums (deterministic chunked order); S = E_last + sum_last
-  double ls = 0.0;
-  for (int b = b0; b < b1; ++b) ls = ls + KP[b].sum;
-  double wi = wave_incl_sum(ls);
-  if (lane == 63) sv[wv] = wi;
-  __syncthreads();
-  double pre = 0.0;
-  for (int w = 0; w < wv; ++w) pre = pre + sv[w];
-  // exclusive prefix of this thread's chunk: previous waves + the previous lane's inclusive value
-  const double prev_incl = __shfl_up(wi, 1, 64);
-  double e = lane == 0 ? pre : pre + prev_incl;
-  for (int b = b0; b < b1; ++b) {
-    Eb[b] = e;
-    e = e + KP[b].sum;
-  }
-  if (b1 == nblk && b0 < b1) s_S = e;
-  if (nblk == 0 && tid == 0) s_S = 0.0;
-  __syncthreads();
-  const double S = s_S;
-
-  // exclusive max-scan of per-block max normalised cumulative weight
-  double lm = -INFINITY;
-  if (S != 0.0)
-    for (int b = b0; b < b1; ++b) {
-      const double c = (Eb[b] + (S > 0.0 ? KP[b].maxrel : KP[b].minrel)) / S;
-      lm = c > lm ? c : lm;
-    }
-  const double wm = wave_incl_max(lm);
-  __syncthreads();
-  if (lane == 63) sv2[wv] = wm;
-  __syncthreads();
-  double pm = -INFINITY;
-  for (int w = 0; w < wv; ++w) pm = sv2[w] > pm ? sv2[w] : pm;
+// ---- top wave of k_propagate_weigh: iteration bookkeeping, exit rule, group prefixes, accept
+template <typename T, int RNG>
+__device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __restrict__ ctrl, int iter,
+                              const GroupPart* __restrict__ gp0, const GroupPart* __restrict__ gp1,
+                              GroupScan* __restrict__ gscan) {
+  const int lane = lane_id();
+  const int ngrp = fa.ngrp;
+  const int slot = c0.cur_slot;
+  // this iteration's max / first argmax
+  double mv = -INFINITY;
+  int mi = 0x7fffffff;
   {
-    const double prev = __shfl_up(wm, 1, 64);
-    if (lane > 0 && prev > pm) pm = prev;
+    const GroupPart* P = slot ? gp1 : gp0;
+    for (int g = lane; g < ngrp; g += 64) cmb_max(mv, mi, ld_wt_d(&P[g].maxw), lo32(ld_wt(&P[g].argmax)));
+    wave_argmax(mv, mi);
   }
-  double run = pm;
-  for (int b = b0; b < b1; ++b) {
-    Rin[b] = run;
-    if (S != 0.0) {
-      const double c = (Eb[b] + (S > 0.0 ? KP[b].maxrel : KP[b].minrel)) / S;
-      run = c > run ? c : run;
+  Ctrl c = c0;
+  if (mv > c.best_max) {  // strict: PE:608
+    c.best_max = mv;
+    c.best_idx = mi;
+    c.best_iter = iter;
+    c.best_slot = slot;
+    c.has_best = 1;
+  }
+  c.iters = iter + 1;
+  const bool go_on = fa.force_iters > 0 ? (c.iters < fa.force_iters)
+                                        : (c.iters < fa.max_iter && mv < fa.exit_thr);  // PE:616
+  c.cur_slot = c.has_best ? 1 - c.best_slot : 1 - slot;
+  if (go_on) {
+    if (lane == 0) *ctrl = c;
+    return;
+  }
+  c.done = 1;
+  c.kept_slot = c.has_best ? c.best_slot : slot;
+  c.kept_iter = c.has_best ? c.best_iter : iter;
+  const GroupPart* KG = c.kept_slot ? gp1 : gp0;
+
+  // group prefixes G_g (tiles of 64 groups, carried), S = total
+  double carry = 0.0;
+  for (int base = 0; base < ngrp; base += 64) {
+    const int g = base + lane;
+    const double s = g < ngrp ? ld_wt_d(&KG[g].sum) : 0.0;
+    const double incl = wave_incl_sum(s);
+    const double prev = __shfl_up(incl, 1, 64);
+    const double G = lane == 0 ? carry : carry + prev;
+    if (g < ngrp) gscan[g].G = G;
+    carry = carry + __shfl(incl, 63, 64);
+  }
+  const double S = carry;
+  // running max of c at each group start: Gin_g = max over earlier groups of fl(fl(G + z)/S)
+  double run = -INFINITY;
+  if (S != 0.0) {
+    for (int base = 0; base < ngrp; base += 64) {
+      const int g = base + lane;
+      double cm = -INFINITY;
+      if (g < ngrp) {
+        const double z = S > 0.0 ? ld_wt_d(&KG[g].zmax) : ld_wt_d(&KG[g].zmin);
+        cm = (gscan[g].G + z) / S;
+      }
+      const double im = wave_incl_max(cm);
+      double ex = lane == 0 ? -INFINITY : __shfl_up(im, 1, 64);
+      ex = ex > run ? ex : run;
+      if (g < ngrp) gscan[g].Gin = ex;
+      const double tm = __shfl(im, 63, 64);
+      run = tm > run ? tm : run;
     }
   }
-  double gmax = -INFINITY;
-  for (int w = 0; w < W; ++w) gmax = sv2[w] > gmax ? sv2[w] : gmax;
-
   // kept iteration's argmax / argmin (re-init branch, PE:714)
   double amv = -INFINITY, anv = INFINITY;
   int ami = 0x7fffffff, ani = 0x7fffffff;
-  for (int b = b0; b < b1; ++b) {
-    cmb_max(amv, ami, KP[b].maxw, KP[b].argmax);
-    cmb_min(anv, ani, KP[b].minw, KP[b].argmin);
+  for (int g = lane; g < ngrp; g += 64) {
+    const uint64_t ai = ld_wt(&KG[g].argmax);
+    cmb_max(amv, ami, ld_wt_d(&KG[g].maxw), lo32(ai));
+    cmb_min(anv, ani, ld_wt_d(&KG[g].minw), hi32(ai));
   }
   wave_argmax(amv, ami);
   wave_argmin(anv, ani);
-  __syncthreads();
   if (lane == 0) {
-    sv[wv] = amv;
-    si[wv] = ami;
-    sv2[wv] = anv;
-    si2[wv] = ani;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < W; ++w) {
-      cmb_max(amv, ami, sv[w], si[w]);
-      cmb_min(anv, ani, sv2[w], si2[w]);
-    }
-    Ctrl c = *ctrl;
     const double highest = c.has_best ? c.best_max : 0.0;
     c.S = S;
-    c.Rmax = gmax;
+    c.Rmax = run;
     c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
     if (c.accepted) {
       c.most_likely_idx = c.best_idx;
-      c.K_total = count_targets<RNG>(fa, c.iters, gmax);
+      c.K_total = count_targets<T, RNG>(fa, c.iters, run);
     } else {
       // argmax of the normalised weights (PE:714): a negative sum flips the order
       c.most_likely_idx = (S < 0.0) ? ani : ami;
@@ -764,45 +794,237 @@ __global__ __launch_bounds__(kReduceThreads) void k_iter_reduce(const FrameArgs 
   }
 }
 
-// ---- stratified resampling: scan + target counts + wave-cooperative scatter of regenerated particles
-template <typename T, int RNG>
+// ---- launch 1: motion + projection + likelihood, one particle per thread
+template <typename T, int RNG, int MAXM, bool PRUNE>
+__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
+    const FrameArgsT<T> fa, const double* __restrict__ blobs, const T* __restrict__ prior, T* __restrict__ w0,
+    T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, int iter, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ double s_tot[kWaves], s_rmax[kWaves], s_rmin[kWaves], s_mx[kWaves], s_mn[kWaves];
+  __shared__ int s_ix[kWaves], s_in[kWaves];
+
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
+  const Ctrl c0 = *ctrl;
+  if (c0.done) return;  // the exit rule already fired (uniform)
+  const int slot = c0.cur_slot;
+  const LdsBlobs<T> tb = build_blob_table<T>(fa, blobs, smem);
+
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  T w = (T)0;
+  if (valid) {
+    T P[12], u[MAXM], v[MAXM];
+    make_particle<T, RNG>(fa, prior, n, iter, P);
+    project_markers<T, MAXM>(fa, P, u, v);
+    if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
+      T m[MAXM];
+      int r[MAXM];
+      column_minima<T, MAXM, PRUNE>(fa, u, v, tb.bx, tb.by, tb.orig, tb.bstart, tb.xmin, tb.inv_bw, m, r);
+      w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
+    }
+    (slot ? w1 : w0)[n] = w;
+  }
+  // wave partials: scan total, extrema of the wave-inclusive prefix, max/argmax, min/argmin
+  const double wd = valid ? (double)w : 0.0;
+  const double wi = wave_incl_sum(wd);
+  const double rmx = wave_max(valid ? wi : -INFINITY);
+  const double rmn = wave_min(valid ? wi : INFINITY);
+  T mx = valid ? w : -inf_t<T>(), mn = valid ? w : inf_t<T>();
+  int ix = valid ? n : 0x7fffffff, in_ = ix;
+  wave_argmax(mx, ix);
+  wave_argmin(mn, in_);
+  const int lane = lane_id(), wv = wave_id();
+  if (lane == 63) s_tot[wv] = wi;
+  if (lane == 0) {
+    s_rmax[wv] = rmx;
+    s_rmin[wv] = rmn;
+    s_mx[wv] = (double)mx;
+    s_mn[wv] = (double)mn;
+    s_ix[wv] = ix;
+    s_in[wv] = in_;
+  }
+  __syncthreads();
+  if (wv != 0) return;  // waves 1..3 are done; wave 0 publishes and (maybe) reduces
+
+  const int g = blockIdx.x / kGroup;
+  const int gsize = min(kGroup, fa.nblk - g * kGroup);
+  int last = 0;
+  if (lane == 0) {
+    // block partial, same association as block_incl_sum: pre_w = ((0 + t0) + t1) + ...
+    double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = s_mx[0], bmn = s_mn[0];
+    int bix = s_ix[0], bin = s_in[0];
+#pragma unroll
+    for (int ww = 0; ww < kWaves; ++ww) {
+      const double a = pre + s_rmax[ww], b = pre + s_rmin[ww];
+      maxrel = a > maxrel ? a : maxrel;
+      minrel = b < minrel ? b : minrel;
+      if (ww) {
+        cmb_max(bmx, bix, s_mx[ww], s_ix[ww]);
+        cmb_min(bmn, bin, s_mn[ww], s_in[ww]);
+      }
+      pre = pre + s_tot[ww];
+    }
+    BlockPart* bp = (slot ? part1 : part0) + blockIdx.x;
+    st_wt_d(&bp->sum, pre);
+    st_wt_d(&bp->maxrel, maxrel);
+    st_wt_d(&bp->minrel, minrel);
+    st_wt_d(&bp->maxw, bmx);
+    st_wt_d(&bp->minw, bmn);
+    st_wt(&bp->argmax, pack2(bix, bin));
+    if (stamps) stamp_max(stamps, 1, rt_now());
+    last = arrive_last(gcount + g, gsize) ? 1 : 0;
+  }
+  if (!__shfl(last, 0, 64)) return;
+  propagate_group(fa.nblk, g, slot ? part1 : part0, slot ? bscan1 : bscan0, slot ? gpart1 : gpart0);
+  if (!wave_arrive_last(tcount, fa.ngrp)) return;
+  if (stamps && lane == 0) stamps[2] = rt_now();
+  propagate_top<T, RNG>(fa, c0, ctrl, iter, gpart0, gpart1, gscan);
+  if (stamps && lane == 0) stamps[3] = rt_now();
+}
+
+// ---- winner + frame record (one wave).  Writes into pinned host memory, then resets the control
+// record for the next frame.
+template <typename T, int RNG, int MAXM>
+__device__ void finalize_frame(const FrameArgsT<T>& fa, const Ctrl& c, Ctrl* __restrict__ ctrl,
+                               const double* __restrict__ blobs, const T* __restrict__ prior, int winner,
+                               OutDev* __restrict__ out) {
+  const int lane = lane_id();
+  T Pm[12], P[12];
+  make_particle<T, RNG>(fa, prior, c.most_likely_idx, c.kept_iter, Pm);
+  int np = 0;
+  uint32_t pairs[2 * MAXM];
+  if (c.accepted) {
+    make_particle<T, RNG>(fa, prior, winner, c.kept_iter, P);
+    T u[MAXM], v[MAXM], m[MAXM];
+    int r[MAXM];
+    project_markers<T, MAXM>(fa, P, u, v);
+    // column minima of the winner, blobs spread over the lanes (first index on ties)
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      T best = inf_t<T>();
+      int arg = 0x7fffffff;
+      if (j < fa.M)
+        for (int i = lane; i < fa.B; i += 64) {
+          const T dx = (T)blobs[2 * i] - u[j];
+          const T dy = (T)blobs[2 * i + 1] - v[j];
+          const T d = fmadd(dx, dx, dy * dy);
+          if (d < best) {
+            best = d;
+            arg = i;
+          }
+        }
+      wave_argmin(best, arg);
+      m[j] = best;
+      r[j] = arg == 0x7fffffff ? 0 : arg;
+    }
+    if (fa.B > 0 && !nan_at_origin((T)blobs[0], (T)blobs[1], u[0], v[0]))
+      score_minima<T, MAXM, true>(fa, m, r, pairs, &np);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) P[q] = Pm[q];
+  }
+  if (lane != 0) return;
+  out->kept_slot = c.kept_slot;
+  out->iters = c.iters;
+  out->kept_iter = c.kept_iter;
+  out->most_likely_idx = c.most_likely_idx;
+  out->accepted = c.accepted;
+  out->resampled = c.accepted;
+  out->winner_idx = c.accepted ? winner : -1;
+  out->flag_fail = c.accepted ? 1 : 4;
+  out->highest_prob = c.has_best ? c.best_max : 0.0;
+  out->prob_sum = c.S;
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    out->most_likely_pose[q] = (double)Pm[q];
+    out->winner_pose[q] = (double)P[q];
+  }
+#pragma unroll
+  for (int q = 0; q < 2 * MAXM; ++q) out->corr[q] = q < 2 * np ? pairs[q] : 0u;
+  for (int q = 2 * MAXM; q < 2 * kMaxMarkers; ++q) out->corr[q] = 0u;
+  out->n_corr = np;
+  __threadfence_system();
+  out->done = 1;
+  __threadfence_system();
+  // the next frame starts from the all-zero control record
+  Ctrl z;
+  z.best_max = 0.0;
+  z.S = 0.0;
+  z.Rmax = 0.0;
+  z.done = z.has_best = z.best_idx = z.best_iter = z.best_slot = z.cur_slot = 0;
+  z.iters = z.kept_slot = z.kept_iter = z.accepted = z.most_likely_idx = z.pad0 = 0;
+  z.K_total = 0;
+  *ctrl = z;
+}
+
+// ---- launch 2: stratified resampling: scan + target counts + wave-cooperative scatter of regenerated
+// particles; the last group's wave picks the winner and writes the frame record
+template <typename T, int RNG, int MAXM>
 __global__ __launch_bounds__(kBlock) void k_resample(
-    const FrameArgs fa, const Ctrl* __restrict__ ctrl, const T* __restrict__ prior, T* __restrict__ post,
-    const T* __restrict__ w0, const T* __restrict__ w1, const double* __restrict__ Eb,
-    const double* __restrict__ Rin, CountPart* __restrict__ cparts, uint32_t* __restrict__ counts) {
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const double* __restrict__ blobs, const T* __restrict__ prior,
+    T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+    const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
+    CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
+    uint32_t* __restrict__ counts, OutDev* __restrict__ out, uint64_t* __restrict__ stamps) {
   __shared__ double s_sum[kWaves];
   __shared__ double s_max[kWaves];
   __shared__ int s_hi[kWaves];
   __shared__ int s_c[kWaves], s_ci[kWaves];
 
-  if (!ctrl->done || !ctrl->accepted) return;
-  const int slot = ctrl->kept_slot, kiter = ctrl->kept_iter, iters = ctrl->iters;
-  const double S = ctrl->S;
-  const int64_t Kt = ctrl->K_total;
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
+  const Ctrl c = *ctrl;
+  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      out->done = 0;
+      __threadfence_system();
+    }
+    return;
+  }
+  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
+    if (blockIdx.x == 0 && threadIdx.x < 64) finalize_frame<T, RNG, MAXM>(fa, c, ctrl, blobs, prior, -1, out);
+    return;
+  }
+  const int slot = c.kept_slot, kiter = c.kept_iter, iters = c.iters;
+  const double S = c.S;
+  const int64_t Kt = c.K_total;
   const int N = fa.N;
   const int blk = blockIdx.x, lane = lane_id(), wv = wave_id();
+  const int g = blk / kGroup;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < N;
   const T* W = slot ? w1 : w0;
+  const BlockScan bs = (slot ? bscan1 : bscan0)[blk];
+  const GroupScan gs = gscan[g];
 
   const double wd = valid ? (double)W[n] : 0.0;
-  double incl, tot;
-  block_incl_sum(wd, incl, tot, s_sum);
-  const double c = (Eb[blk] + incl) / S;
-  // inclusive running max over the block, seeded by the running max of all earlier blocks
-  double rm = wave_incl_max(valid ? c : -INFINITY);
+  double incl;
+  block_incl_sum(wd, incl, s_sum);
+  const double cn = (gs.G + (bs.E + incl)) / S;
+  // running max of c seeded by the exact running max at the block start:
+  // max(Gin_g, fl(fl(G_g + zin_b)/S)); zin_b = -inf (S > 0) / +inf (S < 0) for a group's first block
+  const double zin = S > 0.0 ? bs.zin_max : bs.zin_min;
+  const bool first_in_group = (blk % kGroup) == 0;
+  double rin = gs.Gin;
+  if (!first_in_group) {
+    const double cz = (gs.G + zin) / S;
+    rin = cz > rin ? cz : rin;
+  }
+  const double rm = wave_incl_max(valid ? cn : -INFINITY);
   if (lane == 63) s_max[wv] = rm;
   __syncthreads();
-  double pm = Rin[blk];
+  double pm = rin;
   for (int w = 0; w < wv; ++w) pm = s_max[w] > pm ? s_max[w] : pm;
   const double R = rm > pm ? rm : pm;
-  const int hi = valid ? (int)count_targets<RNG>(fa, iters, R) : N;
+  const int hi = valid ? (int)count_targets<T, RNG>(fa, iters, R) : N;
   if (lane == 63) s_hi[wv] = hi;
   __syncthreads();
   int lo = __shfl_up(hi, 1, 64);
-  if (lane == 0) lo = (wv == 0) ? (int)count_targets<RNG>(fa, iters, Rin[blk]) : s_hi[wv - 1];
-  const int cnt = valid ? hi - lo : 0;
-  if (counts && valid) counts[n] = (uint32_t)cnt;
+  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : s_hi[wv - 1];
+  const int cntn = valid ? hi - lo : 0;
+  if (counts && valid) counts[n] = (uint32_t)cntn;
 
   // write range [a, e): targets past K_total find nothing and copy the last found particle (the
   // reference keeps the previous Particle_index, PE:681)
@@ -822,22 +1044,13 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     e = hi;
   }
 
-  // block max count, first index (winner candidates)
-  {
-    double cv = valid ? (double)cnt : -1.0;
+  {  // block max count, first index (winner candidates)
+    int cv = valid ? cntn : -1;
     int ci = valid ? n : 0x7fffffff;
     wave_argmax(cv, ci);
     if (lane == 0) {
-      s_c[wv] = (int)cv;
+      s_c[wv] = cv;
       s_ci[wv] = ci;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double bv = s_c[0];
-      int bi = s_ci[0];
-      for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, (double)s_c[w], s_ci[w]);
-      cparts[blk].maxcount = (int)bv;
-      cparts[blk].idx = bi;
     }
   }
 
@@ -866,64 +1079,40 @@ __global__ __launch_bounds__(kBlock) void k_resample(
       for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = Q[q];
     }
   }
-}
 
-// ---- winner selection + output record (1 block)
-template <typename T, int RNG, int MAXM>
-__global__ __launch_bounds__(kBlock) void k_final(const FrameArgs fa, const Ctrl* __restrict__ ctrl,
-                                                  const T* __restrict__ prior,
-                                                  const CountPart* __restrict__ cparts,
-                                                  const BlobTable<T>* __restrict__ tab,
-                                                  OutDev* __restrict__ out) {
-  __shared__ double sv[kWaves];
-  __shared__ int si[kWaves];
-  const Ctrl c = *ctrl;
-  if (!c.done) {
-    if (threadIdx.x == 0) out->done = 0;
-    return;
-  }
-  double bv = -1.0;
-  int bi = 0x7fffffff;
-  if (c.accepted)
-    for (int b = threadIdx.x; b < fa.nblk; b += kBlock) cmb_max(bv, bi, (double)cparts[b].maxcount, cparts[b].idx);
-  wave_argmax(bv, bi);
-  if (lane_id() == 0) {
-    sv[wave_id()] = bv;
-    si[wave_id()] = bi;
-  }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sv[w], si[w]);
-
-  OutDev o;
-  o.done = 1;
-  o.pad = 0;
-  o.iters = c.iters;
-  o.kept_iter = c.kept_iter;
-  o.most_likely_idx = c.most_likely_idx;
-  o.accepted = c.accepted;
-  o.resampled = c.accepted;
-  o.winner_idx = c.accepted ? bi : -1;
-  o.flag_fail = c.accepted ? 1 : 4;
-  o.highest_prob = c.has_best ? c.best_max : 0.0;
-  o.prob_sum = c.S;
-  o.n_corr = 0;
-  for (int q = 0; q < 2 * kMaxMarkers; ++q) o.corr[q] = 0u;
-
-  T P[12];
-  make_particle<T, RNG>(fa, prior, c.most_likely_idx, c.kept_iter, P);
-  for (int q = 0; q < 12; ++q) o.most_likely_pose[q] = (double)P[q];
-  if (c.accepted) {
-    make_particle<T, RNG>(fa, prior, bi, c.kept_iter, P);
-    T u[MAXM], v[MAXM];
-    project_markers<T, MAXM>(fa, P, u, v);
-    int np = 0;
-    likelihood<T, MAXM, true, true>(fa, u, v, tab->bx, tab->by, tab->orig, tab->bstart, tab->xmin,
-                                    tab->inv_bw, tab->b0x, tab->b0y, tab->tolq, o.corr, &np);
-    o.n_corr = np;
+  if (wv != 0) return;
+  int last = 0;
+  if (lane == 0) {
+    int bv = s_c[0], bi = s_ci[0];
+    for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, s_c[w], s_ci[w]);
+    st_wt(cpart + blk, pack2(bv, bi));
+    if (stamps) stamp_max(stamps, 5, rt_now());
+    last = arrive_last(gcount + g, min(kGroup, fa.nblk - g * kGroup)) ? 1 : 0;
   }
-  for (int q = 0; q < 12; ++q) o.winner_pose[q] = (double)P[q];
-  *out = o;
+  if (!__shfl(last, 0, 64)) return;
+  {  // group: max count over its blocks
+    const int b = g * kGroup + lane;
+    int bv = -1, bi = 0x7fffffff;
+    if (b < fa.nblk) {
+      const uint64_t cp = ld_wt(cpart + b);
+      bv = lo32(cp);
+      bi = hi32(cp);
+    }
+    wave_argmax(bv, bi);
+    if (lane == 0) st_wt(cgroup + g, pack2(bv, bi));
+  }
+  if (!wave_arrive_last(tcount, fa.ngrp)) return;
+  if (stamps && lane == 0) stamps[6] = rt_now();
+  // winner = argmax resample count, first index (PE:685-686)
+  int bv = -1, bi = 0x7fffffff;
+  for (int gg = lane; gg < fa.ngrp; gg += 64) {
+    const uint64_t cp = ld_wt(cgroup + gg);
+    cmb_max(bv, bi, lo32(cp), hi32(cp));
+  }
+  wave_argmax(bv, bi);
+  finalize_frame<T, RNG, MAXM>(fa, c, ctrl, blobs, prior, bi, out);
+  if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path)
@@ -940,20 +1129,19 @@ __global__ void k_export(const T* __restrict__ st, double* __restrict__ poses, i
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)st[(int64_t)q * ld + n];
 }
 template <typename T, int RNG>
-__global__ void k_regen(const FrameArgs fa, const Ctrl* __restrict__ ctrl, const T* __restrict__ prior,
+__global__ void k_regen(const FrameArgsT<T> fa, int kept_iter, const T* __restrict__ prior,
                         double* __restrict__ poses) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= fa.N) return;
   T P[12];
-  make_particle<T, RNG>(fa, prior, n, ctrl->kept_iter, P);
+  make_particle<T, RNG>(fa, prior, n, kept_iter, P);
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)P[q];
 }
 template <typename T>
-__global__ void k_weights_export(const Ctrl* __restrict__ ctrl, const T* __restrict__ w0,
-                                 const T* __restrict__ w1, double* __restrict__ out, int N) {
+__global__ void k_weights_export(const T* __restrict__ w, double* __restrict__ out, int N) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  out[n] = (double)(ctrl->kept_slot ? w1 : w0)[n];
+  out[n] = (double)w[n];
 }
 
 }  // namespace pfmpe

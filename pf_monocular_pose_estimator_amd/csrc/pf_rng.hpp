@@ -106,6 +106,26 @@ PF_HD double u53(uint32_t x0, uint32_t x1) {
   return ((double)(x0 >> 5) * 67108864.0 + (double)(x1 >> 6)) * (1.0 / 9007199254740992.0);
 }
 
-enum : uint32_t { kTagMotionA = 0u, kTagMotionB = 1u, kTagResample = 2u };
+enum : uint32_t { kTagMotion = 0u, kTagResample = 2u };
+
+// Motion draws: ONE Philox4x32-10 call per (particle, iteration) yields the six 21-bit uniforms
+// (angX, angY, angZ, tX, tY, tZ): the top 21 bits of each output word, then two more built from the
+// low 11 bits.  k * 2^-21 is exact in float and double.
+struct Draws6 {
+  uint32_t v[6];
+};
+PF_HD Draws6 philox_motion6(uint32_t n, uint32_t iter, uint32_t flo, uint32_t fhi, uint32_t k0, uint32_t k1) {
+  const U32x4 o = philox4x32_10(n, iter | (kTagMotion << 24), flo, fhi, k0, k1);
+  Draws6 d;
+  d.v[0] = o.x >> 11;
+  d.v[1] = o.y >> 11;
+  d.v[2] = o.z >> 11;
+  d.v[3] = o.w >> 11;
+  d.v[4] = ((o.x & 0x7FFu) << 10) | (o.y & 0x3FFu);
+  d.v[5] = ((o.z & 0x7FFu) << 10) | (o.w & 0x3FFu);
+  return d;
+}
+PF_HD float u21f(uint32_t v) { return (float)v * (1.0f / 2097152.0f); }
+PF_HD double u21d(uint32_t v) { return (double)v * (1.0 / 2097152.0); }
 
 }  // namespace pfmpe

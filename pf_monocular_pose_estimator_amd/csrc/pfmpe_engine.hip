@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,6 +21,8 @@
 using namespace pfmpe;
 
 static_assert(sizeof(OutDev) == 8 + sizeof(pfmpe_frame_out), "OutDev must mirror pfmpe_frame_out");
+static_assert(offsetof(OutDev, corr) == 8 + offsetof(pfmpe_frame_out, corr), "OutDev layout");
+static_assert(offsetof(OutDev, iters) == 8, "OutDev layout");
 static_assert(PFMPE_MAX_MARKERS == kMaxMarkers, "marker capacity mismatch");
 static_assert(PFMPE_MAX_BLOBS == kMaxBlobs, "blob capacity mismatch");
 
@@ -39,20 +42,24 @@ struct pfmpe_ctx {
   void* d_state[2] = {nullptr, nullptr};
   int prior_idx = 0;
   void* d_w[2] = {nullptr, nullptr};
+  int max_grp = 0;
   BlockPart* d_part[2] = {nullptr, nullptr};
-  double* d_Eb = nullptr;
-  double* d_Rin = nullptr;
-  CountPart* d_cparts = nullptr;
-  void* d_table = nullptr;
+  BlockScan* d_bscan[2] = {nullptr, nullptr};
+  GroupPart* d_gpart[2] = {nullptr, nullptr};
+  GroupScan* d_gscan = nullptr;
+  CountPart* d_cpart = nullptr;
+  CountPart* d_cgroup = nullptr;
+  uint32_t* d_counters = nullptr;  // [prop group x max_grp][prop top][res group x max_grp][res top]
   Ctrl* d_ctrl = nullptr;
-  OutDev* d_out = nullptr;
-  OutDev* h_out = nullptr;       // pinned
+  OutDev* h_out = nullptr;       // pinned host memory, written by the final wave
+  OutDev* d_out = nullptr;       // its device address
   double* d_blobs = nullptr;
   double* h_blobs = nullptr;     // pinned staging
   double* d_bank = nullptr;
   std::vector<int32_t> bank_off;
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
+  uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
 
   // model / params
   int M = 0;
@@ -68,12 +75,15 @@ struct pfmpe_ctx {
   bool record_counts = false;
   bool prune = true;
   bool timing = false;
+  int diag = 0;
 
   // last step (for get_particles / get_weights)
-  FrameArgs last_fa{};
+  FrameArgsT<float> last_fa_f{};
+  FrameArgsT<double> last_fa_d{};
   bool has_last = false;
   int last_prior_idx = 0;
   bool last_accepted = false;
+  int last_kept_slot = 0, last_kept_iter = 0;
 
   // timing
   std::vector<EventPair> ev_pool;
@@ -136,6 +146,28 @@ int harvest_timing(pfmpe_ctx* c) {
   return PFMPE_OK;
 }
 
+// Wait for the frame record: the final block writes it into pinned host memory (then a system-scope
+// fence and the `done` word), so the host spins on that word instead of paying a stream synchronize.
+// The spin is bounded by hipStreamQuery: an idle stream without a record is an error.
+int wait_frame(pfmpe_ctx* c) {
+  volatile int32_t* done = &c->h_out->done;
+  for (uint64_t spin = 0;; ++spin) {
+    if (*done != -1) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // record loads may not move above the flag load
+      return PFMPE_OK;
+    }
+    if ((spin & 1023u) == 1023u) {
+      const hipError_t q = hipStreamQuery(c->stream);
+      if (q == hipSuccess) {
+        if (*done != -1) return PFMPE_OK;
+        return fail(c, PFMPE_E_HIP, "frame record was not written");
+      }
+      if (q != hipErrorNotReady) return fail(c, PFMPE_E_HIP, std::string("stream error: ") + hipGetErrorString(q));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 #define RET(expr)              \
   do {                         \
     int r_ = (expr);           \
@@ -143,93 +175,98 @@ int harvest_timing(pfmpe_ctx* c) {
   } while (0)
 
 // ---------------------------------------------------------------------- typed launch sequence
+template <typename T> FrameArgsT<T>& last_args(pfmpe_ctx* c);
+template <> FrameArgsT<float>& last_args<float>(pfmpe_ctx* c) { return c->last_fa_f; }
+template <> FrameArgsT<double>& last_args<double>(pfmpe_ctx* c) { return c->last_fa_d; }
+
 template <typename T, int RNG, int MAXM>
 struct Seq {
-  static int prep(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
-    return launch(c, PFMPE_K_PREP, [&] {
-      hipLaunchKernelGGL((k_prep<T>), dim3(1), dim3(kBlock), 0, c->stream, fa, blobs,
-                         (BlobTable<T>*)c->d_table, c->d_ctrl);
-    });
-  }
-  static int iterate(pfmpe_ctx* c, const FrameArgs& fa, int iter) {
+  static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs, int iter) {
     const T* prior = (const T*)c->d_state[c->prior_idx];
-    RET(launch(c, PFMPE_K_PROPAGATE, [&] {
+    const size_t lds = blob_lds_bytes<T>(fa.B);
+    uint32_t* gcount = c->d_counters;
+    uint32_t* tcount = c->d_counters + c->max_grp;
+    return launch(c, PFMPE_K_PROPAGATE, [&] {
       if (c->prune)
-        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true>), dim3(fa.nblk), dim3(kBlock), 0,
-                           c->stream, fa, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1],
-                           (const BlobTable<T>*)c->d_table, c->d_ctrl, iter);
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
+                           blobs, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
+                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
+                           c->d_stamps);
       else
-        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false>), dim3(fa.nblk), dim3(kBlock), 0,
-                           c->stream, fa, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1],
-                           (const BlobTable<T>*)c->d_table, c->d_ctrl, iter);
-    }));
-    return launch(c, PFMPE_K_REDUCE, [&] {
-      hipLaunchKernelGGL((k_iter_reduce<RNG>), dim3(1), dim3(kReduceThreads), 0, c->stream, fa, c->d_ctrl,
-                         c->d_part[0], c->d_part[1], c->d_Eb, c->d_Rin, iter);
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
+                           blobs, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
+                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
+                           c->d_stamps);
     });
   }
-  static int finish(pfmpe_ctx* c, const FrameArgs& fa) {
+  static int finish(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs) {
     const T* prior = (const T*)c->d_state[c->prior_idx];
     T* post = (T*)c->d_state[1 - c->prior_idx];
+    uint32_t* gcount = c->d_counters + c->max_grp + 1;
+    uint32_t* tcount = c->d_counters + 2 * c->max_grp + 1;
+    *(volatile int32_t*)&c->h_out->done = -1;
     RET(launch(c, PFMPE_K_RESAMPLE, [&] {
-      hipLaunchKernelGGL((k_resample<T, RNG>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl,
-                         prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_Eb, c->d_Rin,
-                         c->d_cparts, c->record_counts ? c->d_counts : nullptr);
+      hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, blobs,
+                         prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
+                         c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
+                         c->record_counts ? c->d_counts : nullptr, c->d_out, c->d_stamps);
     }));
-    RET(launch(c, PFMPE_K_FINAL, [&] {
-      hipLaunchKernelGGL((k_final<T, RNG, MAXM>), dim3(1), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, prior,
-                         c->d_cparts, (const BlobTable<T>*)c->d_table, c->d_out);
-    }));
-    HIPCHK(c, hipMemcpyAsync(c->h_out, c->d_out, sizeof(OutDev), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    RET(wait_frame(c));
+    if (c->timing) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;
   }
-  static int step(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
-    RET(prep(c, fa, blobs));
+  static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs) {
     const int iter_cap = fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter);
     int iter = 0;
-    RET(iterate(c, fa, iter++));
-    RET(finish(c, fa));
+    RET(iterate(c, fa, blobs, iter++));
+    RET(finish(c, fa, blobs));
     // Rare path: the exit rule did not fire on iteration 0.  Later iterations are queued in growing
-    // batches; kernels of iterations past the exit are no-ops (they read ctrl->done).
+    // batches; launches past the exit are no-ops (they read ctrl->done).
     int batch = 1;
     while (!c->h_out->done) {
       if (iter >= iter_cap) return fail(c, PFMPE_E_STATE, "PF iteration loop did not terminate");
-      for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, iter++));
-      RET(finish(c, fa));
+      for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, blobs, iter++));
+      RET(finish(c, fa, blobs));
       batch = std::min(batch * 2, 16);
     }
+    last_args<T>(c) = fa;
     return PFMPE_OK;
   }
-  static int regen(pfmpe_ctx* c, const FrameArgs& fa, const void* prior, double* out) {
-    return launch(c, PFMPE_K_FINAL, [&] {
-      hipLaunchKernelGGL((k_regen<T, RNG>), dim3((fa.N + 255) / 256), dim3(256), 0, c->stream, fa, c->d_ctrl,
+  static int regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
+    const FrameArgsT<T>& fa = last_args<T>(c);
+    return launch(c, PFMPE_K_AUX, [&] {
+      hipLaunchKernelGGL((k_regen<T, RNG>), dim3((fa.N + 255) / 256), dim3(256), 0, c->stream, fa, kept_iter,
                          (const T*)prior, out);
     });
   }
 };
 
+template <typename T>
+FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
+
 template <typename T, int RNG>
-int dispatch_m(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const double* blobs) {
+  const FrameArgsT<T> fa = build_args<T>(c, in);
   if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, blobs);
   return Seq<T, RNG, 16>::step(c, fa, blobs);
 }
 
-int dispatch_step(pfmpe_ctx* c, const FrameArgs& fa, const double* blobs) {
+int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const double* blobs) {
   const bool f64 = c->state_dtype == PFMPE_STATE_F64;
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
-  if (f64) return ref ? dispatch_m<double, kRngReference>(c, fa, blobs) : dispatch_m<double, kRngPhilox>(c, fa, blobs);
-  return ref ? dispatch_m<float, kRngReference>(c, fa, blobs) : dispatch_m<float, kRngPhilox>(c, fa, blobs);
+  if (f64) return ref ? dispatch_m<double, kRngReference>(c, in, blobs) : dispatch_m<double, kRngPhilox>(c, in, blobs);
+  return ref ? dispatch_m<float, kRngReference>(c, in, blobs) : dispatch_m<float, kRngPhilox>(c, in, blobs);
 }
 
-int dispatch_regen(pfmpe_ctx* c, const FrameArgs& fa, const void* prior, double* out) {
+int dispatch_regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
   const bool f64 = c->state_dtype == PFMPE_STATE_F64;
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
-  if (f64) return ref ? Seq<double, kRngReference, 8>::regen(c, fa, prior, out)
-                      : Seq<double, kRngPhilox, 8>::regen(c, fa, prior, out);
-  return ref ? Seq<float, kRngReference, 8>::regen(c, fa, prior, out)
-             : Seq<float, kRngPhilox, 8>::regen(c, fa, prior, out);
+  if (f64) return ref ? Seq<double, kRngReference, 8>::regen(c, kept_iter, prior, out)
+                      : Seq<double, kRngPhilox, 8>::regen(c, kept_iter, prior, out);
+  return ref ? Seq<float, kRngReference, 8>::regen(c, kept_iter, prior, out)
+             : Seq<float, kRngPhilox, 8>::regen(c, kept_iter, prior, out);
 }
+
 
 bool is_identity12(const double* p) {
   static const double I[12] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0};
@@ -238,15 +275,18 @@ bool is_identity12(const double* p) {
   return true;
 }
 
-// FrameArgs from the host state + frame inputs (PE:488-531)
-FrameArgs build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
-  FrameArgs fa{};
-  std::memcpy(fa.cur, in->current_pose, sizeof(fa.cur));
-  std::memcpy(fa.pred, in->predicted_pose, sizeof(fa.pred));
-  std::memcpy(fa.predm, in->prediction, sizeof(fa.predm));
-  std::memcpy(fa.cam, in->cam_move_inv, sizeof(fa.cam));
-  std::memcpy(fa.markers, c->markers, sizeof(fa.markers));
-  std::memcpy(fa.K, c->K, sizeof(fa.K));
+// Kernel arguments from the host state + frame inputs (PE:488-531), pre-converted to T
+template <typename T>
+FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
+  FrameArgsT<T> fa{};
+  for (int q = 0; q < 12; ++q) {
+    fa.cur[q] = (T)in->current_pose[q];
+    fa.pred[q] = (T)in->predicted_pose[q];
+    fa.predm[q] = (T)in->prediction[q];
+    fa.cam[q] = (T)in->cam_move_inv[q];
+  }
+  for (int q = 0; q < kMaxMarkers * 3; ++q) fa.markers[q] = (T)c->markers[q];
+  for (int q = 0; q < 9; ++q) fa.K[q] = (T)c->K[q];
   const pfmpe_params& p = c->params;
   double facT, facR;
   if (in->it_since_init == 1) {  // PE:488-496
@@ -257,14 +297,20 @@ FrameArgs build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
     facR = 0.2;
   }
   for (int q = 0; q < 3; ++q) {
-    fa.lo[q] = p.ang_min * facR;
-    fa.hi[q] = p.ang_max * facR;
-    fa.lo[3 + q] = p.trans_min * facT;
-    fa.hi[3 + q] = p.trans_max * facT;
+    fa.dlo[q] = p.ang_min * facR;
+    fa.dhi[q] = p.ang_max * facR;
+    fa.dlo[3 + q] = p.trans_min * facT;
+    fa.dhi[3 + q] = p.trans_max * facT;
+  }
+  for (int q = 0; q < 6; ++q) {
+    fa.lo[q] = (T)fa.dlo[q];
+    fa.hi[q] = (T)fa.dhi[q];
   }
   fa.growth = p.growth;
-  fa.tol = p.tol;
-  fa.tol_pf = p.tol_pf;
+  fa.tol = (T)p.tol;
+  fa.tol_pf = (T)p.tol_pf;
+  // every blob with sqrt(d2) <= tol_pf (in T arithmetic) has |dx| <= tolq
+  fa.tolq = (T)(p.tol_pf * (1.0 + 1e-3) + 1e-3);
   const int B = in->B;
   fa.exit_thr = (double)((size_t)c->M * (size_t)std::min(p.exit_cap, B));
   fa.accept_thr = (double)((size_t)c->M * (size_t)std::min(p.accept_cap, B));
@@ -282,14 +328,19 @@ FrameArgs build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   fa.max_iter = p.max_iter;
   fa.force_iters = in->force_iters;
   fa.nblk = (c->N + kBlock - 1) / kBlock;
+  fa.ngrp = (fa.nblk + kGroup - 1) / kGroup;
+  fa.diag = c->diag;
   fa.ld = c->ld;
   return fa;
 }
 
+size_t counters_bytes(const pfmpe_ctx* c) { return (size_t)(2 * c->max_grp + 2) * sizeof(uint32_t); }
+
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
-                 c->d_Eb, c->d_Rin, c->d_cparts, c->d_table, c->d_ctrl, c->d_out, c->d_blobs,
-                 c->d_bank, c->d_xfer, c->d_counts};
+                 c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_blobs, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (c->h_out) (void)hipHostFree(c->h_out);
@@ -350,23 +401,27 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bad(PFMPE_E_HIP);
   const size_t state_bytes = (size_t)kPlanes * c->ld * c->es;
   bool ok = true;
+  c->max_grp = (c->max_blk + kGroup - 1) / kGroup;
   for (int i = 0; i < 2; ++i) {
     ok &= hipMalloc(&c->d_state[i], state_bytes) == hipSuccess;
     ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->es) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * sizeof(BlockPart)) == hipSuccess;
+    ok &= hipMalloc((void**)&c->d_bscan[i], (size_t)c->max_blk * sizeof(BlockScan)) == hipSuccess;
+    ok &= hipMalloc((void**)&c->d_gpart[i], (size_t)c->max_grp * sizeof(GroupPart)) == hipSuccess;
   }
-  ok &= hipMalloc((void**)&c->d_Eb, (size_t)c->max_blk * sizeof(double)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_Rin, (size_t)c->max_blk * sizeof(double)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_cparts, (size_t)c->max_blk * sizeof(CountPart)) == hipSuccess;
-  ok &= hipMalloc(&c->d_table, std::max(sizeof(BlobTable<double>), sizeof(BlobTable<float>))) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_gscan, (size_t)c->max_grp * sizeof(GroupScan)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_cpart, (size_t)c->max_blk * sizeof(CountPart)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_cgroup, (size_t)c->max_grp * sizeof(CountPart)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_counters, counters_bytes(c)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_out, sizeof(OutDev)) == hipSuccess;
-  ok &= hipHostMalloc((void**)&c->h_out, sizeof(OutDev), hipHostMallocDefault) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_out, sizeof(OutDev), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+  ok = ok && hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_blobs, (size_t)kMaxBlobs * 2 * sizeof(double)) == hipSuccess;
   ok &= hipHostMalloc((void**)&c->h_blobs, (size_t)kMaxBlobs * 2 * sizeof(double), hipHostMallocDefault) ==
         hipSuccess;
   if (!ok) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_ctrl, 0, sizeof(Ctrl)) != hipSuccess) return bad(PFMPE_E_HIP);
+  if (hipMemset(c->d_counters, 0, counters_bytes(c)) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_state[0], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_state[1], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
   *out = c;
@@ -424,6 +479,13 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
     case PFMPE_OPT_TIMING:
       c->timing = value != 0;
       return PFMPE_OK;
+    case 99:  // undocumented: diagnostic kernel switches for timing experiments
+      c->diag = (int)value;
+      if ((c->diag & 4) && !c->d_stamps) {
+        RET(set_device(c));
+        HIPCHK(c, hipMalloc((void**)&c->d_stamps, 8 * sizeof(uint64_t)));
+      }
+      return PFMPE_OK;
     default:
       return fail(c, PFMPE_E_ARG, "set_option: unknown option");
   }
@@ -448,6 +510,8 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
     hipLaunchKernelGGL((k_import<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
                        (float*)c->d_state[c->prior_idx], N, c->ld);
   HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->N = N;
   c->has_prior = true;
@@ -501,8 +565,7 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     HIPCHK(c, hipMemcpyAsync(c->d_blobs, c->h_blobs, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice,
                              c->stream));
   }
-  const FrameArgs fa = build_args(c, in);
-  RET(dispatch_step(c, fa, blobs));
+  RET(dispatch_step(c, in, blobs));
   if (c->timing) RET(harvest_timing(c));
 
   const OutDev& o = *c->h_out;
@@ -520,10 +583,11 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   std::memcpy(out->most_likely_pose, o.most_likely_pose, sizeof(out->most_likely_pose));
   std::memcpy(out->corr, o.corr, sizeof(out->corr));
 
-  c->last_fa = fa;
   c->has_last = true;
   c->last_prior_idx = c->prior_idx;
   c->last_accepted = o.resampled != 0;
+  c->last_kept_slot = o.kept_slot;
+  c->last_kept_iter = o.kept_iter;
   if (o.resampled) c->prior_idx = 1 - c->prior_idx;  // newPoseEstimation = resampled set (PE:681, 727)
   return PFMPE_OK;
 }
@@ -537,7 +601,7 @@ int pfmpe_get_particles(pfmpe_ctx* c, int which, double* out) {
   RET(ensure_xfer(c));
   const int N = c->N;
   if (which == 0) {
-    RET(dispatch_regen(c, c->last_fa, c->d_state[c->last_prior_idx], c->d_xfer));
+    RET(dispatch_regen(c, c->last_kept_iter, c->d_state[c->last_prior_idx], c->d_xfer));
   } else if (c->state_dtype == PFMPE_STATE_F64) {
     hipLaunchKernelGGL((k_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
                        (const double*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld);
@@ -560,11 +624,11 @@ int pfmpe_get_weights(pfmpe_ctx* c, double* out) {
   RET(ensure_xfer(c));
   const int N = c->N;
   if (c->state_dtype == PFMPE_STATE_F64)
-    hipLaunchKernelGGL((k_weights_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_ctrl,
-                       (const double*)c->d_w[0], (const double*)c->d_w[1], c->d_xfer, N);
+    hipLaunchKernelGGL((k_weights_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
+                       (const double*)c->d_w[c->last_kept_slot], c->d_xfer, N);
   else
-    hipLaunchKernelGGL((k_weights_export<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_ctrl,
-                       (const float*)c->d_w[0], (const float*)c->d_w[1], c->d_xfer, N);
+    hipLaunchKernelGGL((k_weights_export<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
+                       (const float*)c->d_w[c->last_kept_slot], c->d_xfer, N);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, c->d_xfer, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -578,6 +642,20 @@ int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
   if (!c->has_last || !c->last_accepted) return fail(c, PFMPE_E_STATE, "get_counts: last step did not resample");
   RET(set_device(c));
   HIPCHK(c, hipMemcpy(out, c->d_counts, (size_t)c->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return PFMPE_OK;
+}
+
+// Undocumented diagnostic: reset (out == NULL) or read the 8 stamps of the last frame (diag & 4).
+int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
+  if (!c || !c->d_stamps) return PFMPE_E_STATE;
+  RET(set_device(c));
+  if (!out) {
+    uint64_t init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
+    HIPCHK(c, hipMemcpy(c->d_stamps, init, sizeof(init), hipMemcpyHostToDevice));
+    return PFMPE_OK;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(out, c->d_stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return PFMPE_OK;
 }
 
@@ -598,8 +676,7 @@ int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
 }
 
 const char* pfmpe_kernel_name(int kernel) {
-  static const char* names[PFMPE_K_COUNT] = {"k_prep", "k_propagate_weigh", "k_iter_reduce", "k_resample",
-                                             "k_final"};
+  static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux"};
   return (kernel >= 0 && kernel < PFMPE_K_COUNT) ? names[kernel] : "?";
 }
 

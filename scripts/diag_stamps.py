@@ -1,0 +1,23 @@
+import sys, os, ctypes as C
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import pf_monocular_pose_estimator_amd as pf
+from pf_monocular_pose_estimator_amd import synthetic as syn
+lib = pf.load()
+lib.pfmpe_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+for N in [int(x) for x in sys.argv[1:]] or [100000]:
+    cfg = syn.StreamConfig("C2", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 30)
+    eng = pf.Engine(0, N); eng.set_model(st.markers, st.K); eng.set_params(pf.default_params()); eng.set_prior(st.prior())
+    eng.set_option(99, 4)
+    rows = []
+    for fr in st.frames:
+        lib.pfmpe_debug_stamps(eng.ctx, None)
+        eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt, seed=3, frame_idx=fr.index))
+        s = (C.c_uint64 * 8)(); lib.pfmpe_debug_stamps(eng.ctx, s)
+        t = np.array(list(s), dtype=np.float64)
+        t0 = t[0]
+        rows.append([(t[i] - t0) / 100.0 for i in range(8)])  # us (100 MHz)
+    r = np.median(np.array(rows[5:]), axis=0)
+    print(f"N={N}: K1 start 0 | last arrival {r[1]:.2f} | reduce {r[2]:.2f}->{r[3]:.2f} ({r[3]-r[2]:.2f}) || K2 start {r[4]:.2f} | last arrival {r[5]:.2f} | final {r[6]:.2f}->{r[7]:.2f} ({r[7]-r[6]:.2f})  [us]")
+    eng.close()

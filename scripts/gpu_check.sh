@@ -16,7 +16,7 @@ step() {  # step <name> <timeout-s> <cmd...>
 }
 what=${1:-all}
 if [ "$what" = all ] || [ "$what" = tests ]; then
-  step pytest_gpu 1200 python -m pytest tests -m gpu -q -rf --timeout=600 || true
+  step pytest_gpu 700 python -m pytest tests -m gpu -q -rf --timeout=600 || true
 fi
 if [ "$what" = all ] || [ "$what" = smoke ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit 1

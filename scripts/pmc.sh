@@ -1,0 +1,13 @@
+#!/bin/bash
+# PMC passes (each its own rocprofv3 run, no trace domains): pmc.sh <tag> <bench args...>
+cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out; export TMPDIR=/tmp
+tag=$1; shift
+i=0
+for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_WAVE_CYCLES" \
+           "SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_$tag/p$i -o run -- python3 bench.py --cpu-frames 0 --no-timing "$@" > gpurun_out/pmc_${tag}_p$i.log 2>&1
+  rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${tag}_p$i.log; exit $rc; fi
+done
+python3 scripts/pmc_summary.py gpurun_out/pmc_$tag

@@ -104,7 +104,8 @@ def test_fp64_exit_rule_runs_all_iterations(rng):
     st = syn.make_stream(cfg, 1)
     fr = st.frames[0]
     true_px = syn.project(st.K, fr.truth, st.markers)
-    blobs = np.vstack([true_px[1:], fr.blobs[:7]]).astype(np.float32).astype(np.float64)
+    outliers = np.random.default_rng(5).uniform([0, 0], [syn.IMAGE_W, syn.IMAGE_H], size=(7, 2))
+    blobs = np.vstack([true_px[1:], outliers]).astype(np.float32).astype(np.float64)
     prm = pf.default_params()
     prm.rng_mode = RNG[rng]
     eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng])
@@ -148,12 +149,13 @@ def test_no_blobs_reinitialises(state):
     eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX)
     prm = pf.default_params()
     eng.set_prior(st.prior())
-    for blobs in (np.zeros((0, 2)), np.array([[5000.0, 5000.0], [6000.0, -40.0]])):
+    # B = 0: exit threshold M*min(5, B) = 0, so the reference stops after one iteration (PE:616)
+    for blobs, iters in ((np.zeros((0, 2)), 1), (np.array([[5000.0, 5000.0], [6000.0, -40.0]]), 80)):
         out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, st.prior(), fr.current_pose, fr.predicted_pose,
                                        fr.prediction, blobs, seed=9, frame_idx=1)
         assert out["accepted"] == 0 and ref["accepted"] == 0
         assert out["flag_fail"] == pf.FLAG_REINIT
-        assert out["iters"] == ref["iters"] == 80
+        assert out["iters"] == ref["iters"] == iters
         assert out["most_likely_idx"] == ref["most_likely_idx"]
         assert out["winner_idx"] == -1
     eng.close()
@@ -222,9 +224,18 @@ def test_fp64_negative_weights_running_max(rng):
     eng.close()
 
 
+def rotation_angle(R1, R2):
+    c = (np.trace(R1.T @ R2) - 1) / 2
+    return float(np.arccos(np.clip(c, -1, 1)))
+
+
 @pytest.mark.parametrize("rng", ["ref", "philox"])
 @pytest.mark.parametrize("N,M,B,heavy", [(20000, 5, 50, False), (8192, 12, 200, True)])
 def test_fp32_tolerance(rng, N, M, B, heavy):
+    """fp32 throughput path vs the fp64 oracle.  Weights may differ discretely where a marker sits within
+    ~1e-5 px of the tol_PF gate; such a flip shifts every later stratum boundary, so counts are checked
+    against the oracle's resampler run on the GPU's OWN weights (exact), and outputs are checked by the
+    north_star criterion: refined (Gauss-Newton) poses within 1e-4 m / 1e-3 rad."""
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 3)
     prm = pf.default_params()
@@ -233,27 +244,30 @@ def test_fp32_tolerance(rng, N, M, B, heavy):
     eng.set_prior(st.prior())
     for fr in st.frames:
         prior_used = eng.get_particles(1)  # float-representable values: the oracle starts from the same set
+        seed = 50 + fr.index
         out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior_used, fr.current_pose, fr.predicted_pose,
-                                       fr.prediction, fr.blobs, seed=50 + fr.index, frame_idx=fr.index)
+                                       fr.prediction, fr.blobs, seed=seed, frame_idx=fr.index)
         assert out["accepted"] == ref["accepted"]
         assert out["iters"] == ref["iters"]
         dw = np.abs(gpu["weights"] - arr["weights"])
-        assert np.mean(dw <= 2e-3) >= 0.995, np.sort(dw)[-10:]
+        assert np.sum(dw > 2e-3) <= max(3, N // 1000), np.sort(dw)[-10:]
         dp = np.abs(gpu["propagated"] - arr["propagated"])
         assert dp[:, [0, 1, 2, 4, 5, 6, 8, 9, 10]].max() < 1e-5 and dp[:, [3, 7, 11]].max() < 1e-5
         if out["resampled"]:
             c = gpu["counts"].astype(np.int64)
-            assert c.sum() <= N and (c >= 0).all()
-            same = np.mean(c == arr["counts"])
-            assert same >= 0.97, same
-            # the winner has the maximum count (first on ties) and its pose is the propagated particle
+            c_ref, _ = orc.stratified_resample(gpu["weights"], RNG[rng], seed, fr.index, out["iters"])
+            assert np.sum(c != c_ref) <= 2, np.where(c != c_ref)[0][:10]
             w = out["winner_idx"]
             assert c[w] == c.max() and np.argmax(c) == w
             np.testing.assert_allclose(out["winner_pose"], gpu["propagated"][w], atol=1e-6)
-            # correspondences of the winner equal the oracle likelihood evaluated on that pose
             proj = np.array([orc.project(st.K, gpu["propagated"][w], X) for X in st.markers])
             _, pairs = orc.likelihood(proj, fr.blobs, prm.tol, prm.tol_pf)
             assert np.array_equal(out["pairs"], pairs)
+            if np.array_equal(out["pairs"], ref["pairs"]):
+                pg, _, _ = orc.optimise_pose(st.markers, st.K, fr.blobs, out["pairs"], out["winner_pose"])
+                pr, _, _ = orc.optimise_pose(st.markers, st.K, fr.blobs, ref["pairs"], ref["winner_pose"])
+                assert np.abs(pg[[3, 7, 11]] - pr[[3, 7, 11]]).max() < 1e-4
+                assert rotation_angle(syn.to44(pg)[:3, :3], syn.to44(pr)[:3, :3]) < 1e-3
     eng.close()
 
 
