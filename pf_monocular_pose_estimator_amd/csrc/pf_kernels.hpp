@@ -760,7 +760,8 @@ __device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __r
         cm = (gscan[g].G + z) / S;
       }
       const double im = wave_incl_max(cm);
-      double ex = lane == 0 ? -INFINITY : __shfl_up(im, 1, 64);
+      const double im_prev = __shfl_up(im, 1, 64);  // every lane executes the shuffle (no divergence)
+      double ex = lane == 0 ? -INFINITY : im_prev;
       ex = ex > run ? ex : run;
       if (g < ngrp) gscan[g].Gin = ex;
       const double tm = __shfl(im, 63, 64);
