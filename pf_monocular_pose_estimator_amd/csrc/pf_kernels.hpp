@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <math.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "pf_rng.hpp"
@@ -65,6 +66,16 @@ struct FrameArgsT {
   int32_t cam_identity, max_iter, force_iters, nblk;
   int32_t ngrp, diag;             // groups; diagnostic switches (0 in production)
   int64_t ld;                     // SoA plane stride in elements
+};
+
+// The frame-constant arrays, staged once per block into LDS and read from there (broadcast reads):
+// kept in SGPRs they would spill into VGPR lanes and cap residency (MI355X_MICROARCH.md "Residency").
+template <typename T>
+struct LdsConst {
+  T cur[12], pred[12], predm[12], cam[12];
+  T markers[kMaxMarkers * 3];
+  T K[9];
+  T lo[6], hi[6];
 };
 
 // Per-frame control record.  All-zero is the valid "start of frame" state (zeroed at create, set_prior
@@ -104,13 +115,15 @@ struct alignas(8) CountPart {
   int32_t maxcount, idx;
 };
 
-// frame record written by the final wave into pinned host memory (pfmpe_frame_out layout + 2 words)
+// frame record written by the final wave into pinned host memory: the pfmpe_frame_out layout, then the
+// kept slot and the publication tag (2 * frame sequence + finished)
 struct OutDev {
-  int32_t done, kept_slot;
   int32_t iters, kept_iter, most_likely_idx, accepted, resampled, winner_idx, n_corr, flag_fail;
   double highest_prob, prob_sum;
   double winner_pose[12], most_likely_pose[12];
   uint32_t corr[2 * kMaxMarkers];
+  int32_t kept_slot;
+  int32_t tag;
 };
 
 // ----------------------------------------------------------------------------- scalar helpers
@@ -151,6 +164,29 @@ __device__ __forceinline__ T inf_t() {
   return (T)INFINITY;
 }
 
+// thread 0 copies the kernarg arrays (compile-time indices) into LDS; callers barrier afterwards
+template <typename T>
+__device__ __forceinline__ void stage_consts(const FrameArgsT<T>& fa, LdsConst<T>& sc) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      sc.cur[q] = fa.cur[q];
+      sc.pred[q] = fa.pred[q];
+      sc.predm[q] = fa.predm[q];
+      sc.cam[q] = fa.cam[q];
+    }
+#pragma unroll
+    for (int q = 0; q < kMaxMarkers * 3; ++q) sc.markers[q] = fa.markers[q];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) sc.K[q] = fa.K[q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      sc.lo[q] = fa.lo[q];
+      sc.hi[q] = fa.hi[q];
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- pose algebra
 // 3x4 affine compose C = A*B with the reference's full-4x4 summation order (k = 0..3 sequential; the
 // zero bottom-row terms add +0 and are skipped without changing any non-zero value).
@@ -171,16 +207,16 @@ __device__ __forceinline__ void compose(const T* A, const T* B, T* C) {
 
 // The motion model (PE:543-588) for particle n in PF iteration `iter`; P receives the 3x4 pose.
 template <typename T, int RNG>
-__device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const T* __restrict__ prior, int n,
-                                              int iter, T* P) {
+__device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc,
+                                              const T* __restrict__ prior, int n, int iter, T* P) {
   if (n == 0) {  // current_pose_ (PE:547)
 #pragma unroll
-    for (int q = 0; q < 12; ++q) P[q] = fa.cur[q];
+    for (int q = 0; q < 12; ++q) P[q] = sc.cur[q];
     return;
   }
   if (n == 1) {  // predicted_pose_ (PE:551)
 #pragma unroll
-    for (int q = 0; q < 12; ++q) P[q] = fa.pred[q];
+    for (int q = 0; q < 12; ++q) P[q] = sc.pred[q];
     return;
   }
   T A[12];
@@ -189,13 +225,13 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const T* 
   if (fa.it > 1) {
     if (!fa.cam_identity) {  // camMoveInv * prior (PE:556-558)
       T X[12];
-      compose(fa.cam, A, X);
+      compose(sc.cam, A, X);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = X[q];
     }
     if ((iter % 10) != 0) {  // ... * predictionMatrix (PE:556)
       T X[12];
-      compose(A, fa.predm, X);
+      compose(A, sc.predm, X);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = X[q];
     }
@@ -219,20 +255,20 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const T* 
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const T u = (T)u21d(r.v[q]);
-      const T draw = u * (fa.hi[q] - fa.lo[q]) + fa.lo[q];
+      const T draw = u * (sc.hi[q] - sc.lo[q]) + sc.lo[q];
       d[q] = draw * g;
     }
   }
-  T sa, ca, sb, cb, sc, cc;
+  T sa, ca, sb, cb, sz, cz;
   sincos_t(d[0], &sa, &ca);
   sincos_t(d[1], &sb, &cb);
-  sincos_t(d[2], &sc, &cc);
+  sincos_t(d[2], &sz, &cz);
   // R = ((R_A * Rz(c)) * Ry(b)) * Rx(a)   (PE:582)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const T a0 = A[i * 4 + 0], a1 = A[i * 4 + 1], a2 = A[i * 4 + 2];
-    const T z0 = fmadd(a1, sc, a0 * cc);      // A*Rz col 0
-    const T z1 = fmadd(a1, cc, a0 * (-sc));   // A*Rz col 1
+    const T z0 = fmadd(a1, sz, a0 * cz);      // A*Rz col 0
+    const T z1 = fmadd(a1, cz, a0 * (-sz));   // A*Rz col 1
     const T y0 = fmadd(a2, (-sb), z0 * cb);   // *Ry col 0
     const T y2 = fmadd(a2, cb, z0 * sb);      // *Ry col 2
     const T x1 = fmadd(y2, sa, z1 * ca);      // *Rx col 1
@@ -246,22 +282,23 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const T* 
 
 // project2d (PE:1017-1034): p = (K34*T) * [X;1], u = p/p.z — full K, no distortion, no z>0 test
 template <typename T, int MAXM>
-__device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const T* P, T* u, T* v) {
+__device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* P, T* u,
+                                                T* v) {
   T Q[12];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      T s = fa.K[i * 3 + 0] * P[0 * 4 + j];
-      s = fmadd(fa.K[i * 3 + 1], P[1 * 4 + j], s);
-      s = fmadd(fa.K[i * 3 + 2], P[2 * 4 + j], s);
+      T s = sc.K[i * 3 + 0] * P[0 * 4 + j];
+      s = fmadd(sc.K[i * 3 + 1], P[1 * 4 + j], s);
+      s = fmadd(sc.K[i * 3 + 2], P[2 * 4 + j], s);
       Q[i * 4 + j] = s;
     }
   }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     if (j < fa.M) {
-      const T X = fa.markers[3 * j], Y = fa.markers[3 * j + 1], Z = fa.markers[3 * j + 2];
+      const T X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
       T p[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -514,6 +551,18 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
 // write back the XCD's whole dirty L2 (the weights / new prior this kernel streams) once per block.
 typedef __attribute__((address_space(1))) uint64_t gu64_t;
 typedef __attribute__((address_space(1))) uint32_t gu32_t;
+
+// publication to the host (HIP memory model, system scope): relaxed write-through stores of the record,
+// then ONE release store of the tag
+__device__ __forceinline__ void st_sys64(void* p, uint64_t v) {
+  __hip_atomic_store((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys32(void* p, uint32_t v) {
+  __hip_atomic_store((gu32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void publish_tag(int32_t* p, int32_t tag) {
+  __hip_atomic_store((gu32_t*)p, (uint32_t)tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ void st_wt(void* p, uint64_t v) {
   __hip_atomic_store((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -804,6 +853,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
     uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, int iter, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
   __shared__ double s_tot[kWaves], s_rmax[kWaves], s_rmin[kWaves], s_mx[kWaves], s_mn[kWaves];
   __shared__ int s_ix[kWaves], s_in[kWaves];
 
@@ -811,6 +861,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   const Ctrl c0 = *ctrl;
   if (c0.done) return;  // the exit rule already fired (uniform)
   const int slot = c0.cur_slot;
+  stage_consts(fa, sc);  // made visible by the barriers inside build_blob_table
   const LdsBlobs<T> tb = build_blob_table<T>(fa, blobs, smem);
 
   const int n = blockIdx.x * kBlock + threadIdx.x;
@@ -818,8 +869,8 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   T w = (T)0;
   if (valid) {
     T P[12], u[MAXM], v[MAXM];
-    make_particle<T, RNG>(fa, prior, n, iter, P);
-    project_markers<T, MAXM>(fa, P, u, v);
+    make_particle<T, RNG>(fa, sc, prior, n, iter, P);
+    project_markers<T, MAXM>(fa, sc, P, u, v);
     if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
       T m[MAXM];
       int r[MAXM];
@@ -889,19 +940,19 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
 // ---- winner + frame record (one wave).  Writes into pinned host memory, then resets the control
 // record for the next frame.
 template <typename T, int RNG, int MAXM>
-__device__ void finalize_frame(const FrameArgsT<T>& fa, const Ctrl& c, Ctrl* __restrict__ ctrl,
+__device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
                                const double* __restrict__ blobs, const T* __restrict__ prior, int winner,
-                               OutDev* __restrict__ out) {
+                               OutDev& rec, OutDev* __restrict__ out, int32_t tag) {
   const int lane = lane_id();
   T Pm[12], P[12];
-  make_particle<T, RNG>(fa, prior, c.most_likely_idx, c.kept_iter, Pm);
+  make_particle<T, RNG>(fa, sc, prior, c.most_likely_idx, c.kept_iter, Pm);
   int np = 0;
   uint32_t pairs[2 * MAXM];
   if (c.accepted) {
-    make_particle<T, RNG>(fa, prior, winner, c.kept_iter, P);
+    make_particle<T, RNG>(fa, sc, prior, winner, c.kept_iter, P);
     T u[MAXM], v[MAXM], m[MAXM];
     int r[MAXM];
-    project_markers<T, MAXM>(fa, P, u, v);
+    project_markers<T, MAXM>(fa, sc, P, u, v);
     // column minima of the winner, blobs spread over the lanes (first index on ties)
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
@@ -927,29 +978,35 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const Ctrl& c, Ctrl* __r
 #pragma unroll
     for (int q = 0; q < 12; ++q) P[q] = Pm[q];
   }
-  if (lane != 0) return;
-  out->kept_slot = c.kept_slot;
-  out->iters = c.iters;
-  out->kept_iter = c.kept_iter;
-  out->most_likely_idx = c.most_likely_idx;
-  out->accepted = c.accepted;
-  out->resampled = c.accepted;
-  out->winner_idx = c.accepted ? winner : -1;
-  out->flag_fail = c.accepted ? 1 : 4;
-  out->highest_prob = c.has_best ? c.best_max : 0.0;
-  out->prob_sum = c.S;
+  if (lane == 0) {
+    rec.kept_slot = c.kept_slot;
+    rec.iters = c.iters;
+    rec.kept_iter = c.kept_iter;
+    rec.most_likely_idx = c.most_likely_idx;
+    rec.accepted = c.accepted;
+    rec.resampled = c.accepted;
+    rec.winner_idx = c.accepted ? winner : -1;
+    rec.flag_fail = c.accepted ? 1 : 4;
+    rec.highest_prob = c.has_best ? c.best_max : 0.0;
+    rec.prob_sum = c.S;
 #pragma unroll
-  for (int q = 0; q < 12; ++q) {
-    out->most_likely_pose[q] = (double)Pm[q];
-    out->winner_pose[q] = (double)P[q];
+    for (int q = 0; q < 12; ++q) {
+      rec.most_likely_pose[q] = (double)Pm[q];
+      rec.winner_pose[q] = (double)P[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 2 * MAXM; ++q) rec.corr[q] = q < 2 * np ? pairs[q] : 0u;
+    for (int q = 2 * MAXM; q < 2 * kMaxMarkers; ++q) rec.corr[q] = 0u;
+    rec.n_corr = np;
   }
-#pragma unroll
-  for (int q = 0; q < 2 * MAXM; ++q) out->corr[q] = q < 2 * np ? pairs[q] : 0u;
-  for (int q = 2 * MAXM; q < 2 * kMaxMarkers; ++q) out->corr[q] = 0u;
-  out->n_corr = np;
-  __threadfence_system();
-  out->done = 1;
-  __threadfence_system();
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  constexpr int kWords = (int)(offsetof(OutDev, kept_slot) / 8);
+  static_assert(offsetof(OutDev, kept_slot) % 8 == 0 && kWords <= 64, "record layout");
+  if (lane < kWords) st_sys64((uint64_t*)out + lane, ((const uint64_t*)&rec)[lane]);
+  if (lane == kWords) st_sys32(&out->kept_slot, (uint32_t)rec.kept_slot);
+  if (lane != 0) return;
+  publish_tag(&out->tag, tag);
   // the next frame starts from the all-zero control record
   Ctrl z;
   z.best_max = 0.0;
@@ -969,7 +1026,9 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
-    uint32_t* __restrict__ counts, OutDev* __restrict__ out, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  __shared__ LdsConst<T> sc;
+  __shared__ OutDev rec;
   __shared__ double s_sum[kWaves];
   __shared__ double s_max[kWaves];
   __shared__ int s_hi[kWaves];
@@ -978,14 +1037,14 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
   const Ctrl c = *ctrl;
   if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      out->done = 0;
-      __threadfence_system();
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
     return;
   }
+  stage_consts(fa, sc);
+  __syncthreads();
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
-    if (blockIdx.x == 0 && threadIdx.x < 64) finalize_frame<T, RNG, MAXM>(fa, c, ctrl, blobs, prior, -1, out);
+    if (blockIdx.x == 0 && threadIdx.x < 64)
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, blobs, prior, -1, rec, out, 2 * seq + 1);
     return;
   }
   const int slot = c.kept_slot, kiter = c.kept_iter, iters = c.iters;
@@ -1059,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   T P[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) P[q] = (T)0;
-  if (e > a) make_particle<T, RNG>(fa, prior, n, kiter, P);
+  if (e > a) make_particle<T, RNG>(fa, sc, prior, n, kiter, P);
 
   // wave-cooperative scatter: the wave's lanes own consecutive slot ranges [a, e)
   const int wa = __shfl(a, 0, 64);
@@ -1112,7 +1171,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     cmb_max(bv, bi, lo32(cp), hi32(cp));
   }
   wave_argmax(bv, bi);
-  finalize_frame<T, RNG, MAXM>(fa, c, ctrl, blobs, prior, bi, out);
+  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, blobs, prior, bi, rec, out, 2 * seq + 1);
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
@@ -1130,12 +1189,15 @@ __global__ void k_export(const T* __restrict__ st, double* __restrict__ poses, i
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)st[(int64_t)q * ld + n];
 }
 template <typename T, int RNG>
-__global__ void k_regen(const FrameArgsT<T> fa, int kept_iter, const T* __restrict__ prior,
-                        double* __restrict__ poses) {
+__global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int kept_iter, const T* __restrict__ prior,
+                                                 double* __restrict__ poses) {
+  __shared__ LdsConst<T> sc;
+  stage_consts(fa, sc);
+  __syncthreads();
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= fa.N) return;
   T P[12];
-  make_particle<T, RNG>(fa, prior, n, kept_iter, P);
+  make_particle<T, RNG>(fa, sc, prior, n, kept_iter, P);
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)P[q];
 }
 template <typename T>

@@ -20,9 +20,9 @@
 
 using namespace pfmpe;
 
-static_assert(sizeof(OutDev) == 8 + sizeof(pfmpe_frame_out), "OutDev must mirror pfmpe_frame_out");
-static_assert(offsetof(OutDev, corr) == 8 + offsetof(pfmpe_frame_out, corr), "OutDev layout");
-static_assert(offsetof(OutDev, iters) == 8, "OutDev layout");
+static_assert(offsetof(OutDev, kept_slot) == sizeof(pfmpe_frame_out), "OutDev must start with pfmpe_frame_out");
+static_assert(offsetof(OutDev, corr) == offsetof(pfmpe_frame_out, corr), "OutDev layout");
+static_assert(offsetof(OutDev, prob_sum) == offsetof(pfmpe_frame_out, prob_sum), "OutDev layout");
 static_assert(PFMPE_MAX_MARKERS == kMaxMarkers, "marker capacity mismatch");
 static_assert(PFMPE_MAX_BLOBS == kMaxBlobs, "blob capacity mismatch");
 
@@ -53,6 +53,7 @@ struct pfmpe_ctx {
   Ctrl* d_ctrl = nullptr;
   OutDev* h_out = nullptr;       // pinned host memory, written by the final wave
   OutDev* d_out = nullptr;       // its device address
+  int32_t seq = 0;               // frame-record sequence number (publication tag = 2 * seq + finished)
   double* d_blobs = nullptr;
   double* h_blobs = nullptr;     // pinned staging
   double* d_bank = nullptr;
@@ -150,16 +151,21 @@ int harvest_timing(pfmpe_ctx* c) {
 // fence and the `done` word), so the host spins on that word instead of paying a stream synchronize.
 // The spin is bounded by hipStreamQuery: an idle stream without a record is an error.
 int wait_frame(pfmpe_ctx* c) {
-  volatile int32_t* done = &c->h_out->done;
+  volatile int32_t* tag = &c->h_out->tag;
+  const int32_t want = c->seq;
   for (uint64_t spin = 0;; ++spin) {
-    if (*done != -1) {
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // record loads may not move above the flag load
+    const int32_t t = *tag;
+    if ((t >> 1) == want) {
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // record loads may not move above the tag load
       return PFMPE_OK;
     }
     if ((spin & 1023u) == 1023u) {
       const hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) {
-        if (*done != -1) return PFMPE_OK;
+        if ((*tag >> 1) == want) {
+          __atomic_thread_fence(__ATOMIC_ACQUIRE);
+          return PFMPE_OK;
+        }
         return fail(c, PFMPE_E_HIP, "frame record was not written");
       }
       if (q != hipErrorNotReady) return fail(c, PFMPE_E_HIP, std::string("stream error: ") + hipGetErrorString(q));
@@ -167,6 +173,8 @@ int wait_frame(pfmpe_ctx* c) {
     __builtin_ia32_pause();
   }
 }
+
+bool frame_done(const pfmpe_ctx* c) { return (c->h_out->tag & 1) != 0; }
 
 #define RET(expr)              \
   do {                         \
@@ -204,12 +212,13 @@ struct Seq {
     T* post = (T*)c->d_state[1 - c->prior_idx];
     uint32_t* gcount = c->d_counters + c->max_grp + 1;
     uint32_t* tcount = c->d_counters + 2 * c->max_grp + 1;
-    *(volatile int32_t*)&c->h_out->done = -1;
+    c->seq = (c->seq + 1) & 0x3fffffff;
+    const int32_t seq = c->seq;
     RET(launch(c, PFMPE_K_RESAMPLE, [&] {
       hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, blobs,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
-                         c->record_counts ? c->d_counts : nullptr, c->d_out, c->d_stamps);
+                         c->record_counts ? c->d_counts : nullptr, c->d_out, seq, c->d_stamps);
     }));
     RET(wait_frame(c));
     if (c->timing) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
@@ -223,7 +232,7 @@ struct Seq {
     // Rare path: the exit rule did not fire on iteration 0.  Later iterations are queued in growing
     // batches; launches past the exit are no-ops (they read ctrl->done).
     int batch = 1;
-    while (!c->h_out->done) {
+    while (!frame_done(c)) {
       if (iter >= iter_cap) return fail(c, PFMPE_E_STATE, "PF iteration loop did not terminate");
       for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, blobs, iter++));
       RET(finish(c, fa, blobs));
@@ -568,7 +577,7 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   RET(dispatch_step(c, in, blobs));
   if (c->timing) RET(harvest_timing(c));
 
-  const OutDev& o = *c->h_out;
+  const OutDev& o = *(const OutDev*)c->h_out;
   out->iters = o.iters;
   out->kept_iter = o.kept_iter;
   out->most_likely_idx = o.most_likely_idx;

@@ -335,3 +335,23 @@ def test_api_errors_on_gpu():
     with pytest.raises(pf.PFError):
         eng.set_model(np.zeros((17, 3)), syn.K_README)
     eng.close()
+
+
+def test_frame_record_integrity_long_run():
+    """50 consecutive frames: every published record is self-consistent (its pairs are the oracle
+    likelihood pairs of its own winner pose, flags agree) — guards the host-mapped record hand-off."""
+    N = 3000
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 50)
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, pf.RNG_PHILOX)
+    prm = pf.default_params()
+    eng.set_prior(st.prior())
+    for fr in st.frames:
+        out = eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt,
+                                      seed=77 + fr.index, frame_idx=fr.index)).as_dict()
+        assert out["accepted"] == 1 and out["flag_fail"] == pf.FLAG_ACCEPTED and out["resampled"] == 1
+        proj = np.array([orc.project(st.K, out["winner_pose"], X) for X in st.markers])
+        _, pairs = orc.likelihood(proj, fr.blobs, prm.tol, prm.tol_pf)
+        assert np.array_equal(out["pairs"], pairs), fr.index
+        assert out["n_corr"] == len(pairs)
+    eng.close()
