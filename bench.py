@@ -45,7 +45,12 @@ def parse():
     ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    ap.add_argument("--timing-period", type=int, default=8,
+                    help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream)")
     ap.add_argument("--diag", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
+                    "workload; default profiles/pmc_<config>_n<N>.json when present")
+    ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
     return ap.parse_args()
 
 
@@ -56,6 +61,18 @@ def algorithmic_bytes(S: int, N: int) -> dict:
         "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
         "aux": 0,
     }
+
+
+def pmc_traffic(path: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC pass of the same workload (or None)."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            row = json.load(f).get(kernel, {})
+        return row.get("hbm_bytes")
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(cfg, n_frames: int):
@@ -115,22 +132,22 @@ def main():
         eng.step(frames[i])
     eng.reset_kernel_stats()
     if not args.no_timing:
-        eng.set_option(pf.OPT_TIMING, 1)
+        eng.set_option(pf.OPT_TIMING, args.timing_period)
 
     if dist:
         dist.barrier()
+    timed = frames[args.warmup:n_frames]
     t0 = time.perf_counter()
-    updates = 0
-    accepted = 0
-    iters = []
-    for i in range(args.warmup, n_frames):
-        out = eng.step(frames[i])  # blocking: ends with the stream synchronize
-        updates += cfg.N * out.iters
-        iters.append(out.iters)
-        accepted += out.accepted
+    if args.python_loop:
+        outs = [eng.step(f) for f in timed]  # one FFI call per frame
+    else:
+        outs = eng.step_batch(timed)  # the C loop a C++ tracker runs; every frame still blocks on its record
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
+    updates = sum(cfg.N * o.iters for o in outs)
+    iters = [o.iters for o in outs]
+    accepted = sum(o.accepted for o in outs)
     stats = eng.kernel_stats()
     eng.set_option(pf.OPT_TIMING, 0)
 
@@ -155,8 +172,11 @@ def main():
             launches, ms = timed[dom]
             avg_s = ms / 1e3 / launches
             achieved = ab.get(dom, 0) / avg_s / 1e9 if avg_s > 0 else 0.0
+            pmc = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{cfg.name.lower()}_n{cfg.N}.json")
+            traffic = pmc_traffic(pmc, dom)
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                    "traffic": None if traffic is None else round(traffic),
                     "bytes_per_launch": ab.get(dom, 0), "avg_us": round(avg_s * 1e6, 3),
                     "per_kernel_avg_us": {k: round(v[1] * 1e3 / v[0], 3) for k, v in timed.items()}}
         cpu = None

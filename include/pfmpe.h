@@ -133,6 +133,11 @@ int pfmpe_set_prior(pfmpe_ctx* ctx, const double* poses, int N);
  * normalise, accept, stratified-resample, pick the winner.  Blocking. */
 int pfmpe_step(pfmpe_ctx* ctx, const pfmpe_frame_in* in, pfmpe_frame_out* out);
 
+/* n consecutive frames of one stream, in order, each exactly as pfmpe_step (blocking on its own frame
+ * record before the next frame is launched) — the loop a C/C++ tracker runs, without per-call FFI
+ * overhead.  Stops at the first error; *done receives the number of frames completed. */
+int pfmpe_step_batch(pfmpe_ctx* ctx, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out, int* done);
+
 /* getPoseParticles (PE:917, which = 0: kept propagated set of the last step) and getResampledParticles
  * (PE:923, which = 1: current prior).  N x 12 doubles. */
 int pfmpe_get_particles(pfmpe_ctx* ctx, int which, double* out);
@@ -144,7 +149,8 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
 /* Engine options (value semantics in brackets; defaults first):
  *   PFMPE_OPT_RECORD_COUNTS [0|1]  keep counterMeas on device for pfmpe_get_counts
  *   PFMPE_OPT_PRUNE         [1|0]  exact x-window blob pruning in the likelihood (0 = scan all B blobs)
- *   PFMPE_OPT_TIMING        [0|1]  bracket every kernel launch with HIP events (pfmpe_get_kernel_stats) */
+ *   PFMPE_OPT_TIMING        [0|P]  bracket the kernel launches of every P-th frame with HIP events
+ *                                  (pfmpe_get_kernel_stats); P = 1 times every frame, 0 is off */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 

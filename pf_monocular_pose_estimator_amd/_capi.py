@@ -27,7 +27,7 @@ K_PROPAGATE, K_RESAMPLE, K_AUX, K_COUNT = 0, 1, 2, 3
 EXPORTED_SYMBOLS = (
     "pfmpe_create", "pfmpe_destroy", "pfmpe_last_error", "pfmpe_abi_version",
     "pfmpe_set_model", "pfmpe_set_params", "pfmpe_default_params", "pfmpe_set_prior",
-    "pfmpe_step", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
+    "pfmpe_step", "pfmpe_step_batch", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
 )
@@ -102,6 +102,7 @@ def load() -> C.CDLL:
         "pfmpe_default_params": (None, [C.POINTER(Params)]),
         "pfmpe_set_prior": (I, [P, dp, I]),
         "pfmpe_step": (I, [P, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
+        "pfmpe_step_batch": (I, [P, C.POINTER(FrameIn), I, C.POINTER(FrameOut), C.POINTER(I)]),
         "pfmpe_get_particles": (I, [P, I, dp]),
         "pfmpe_get_weights": (I, [P, dp]),
         "pfmpe_get_counts": (I, [P, C.POINTER(C.c_uint32)]),
@@ -225,6 +226,15 @@ class Engine:
         out = FrameOut()
         self._chk(self.lib.pfmpe_step(self.ctx, C.byref(frame), C.byref(out)))
         return out
+
+    def step_batch(self, frames) -> list:
+        """Frames (a list of FrameIn) run back to back in C, each blocking on its own record."""
+        n = len(frames)
+        arr_in = (FrameIn * n)(*frames)
+        arr_out = (FrameOut * n)()
+        done = C.c_int()
+        self._chk(self.lib.pfmpe_step_batch(self.ctx, arr_in, n, arr_out, C.byref(done)))
+        return list(arr_out)
 
     def get_particles(self, which: int) -> np.ndarray:
         out = np.empty((self.N, 12), dtype=np.float64)

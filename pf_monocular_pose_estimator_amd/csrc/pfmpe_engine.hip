@@ -75,7 +75,9 @@ struct pfmpe_ctx {
   // options
   bool record_counts = false;
   bool prune = true;
-  bool timing = false;
+  int timing = 0;          // HIP-event sampling period in frames (0 = off)
+  bool timing_now = false;  // this frame's launches are bracketed
+  int64_t timing_frame = 0;
   int diag = 0;
 
   // last step (for get_particles / get_weights)
@@ -118,7 +120,7 @@ int set_device(pfmpe_ctx* c) {
 template <typename Launch>
 int launch(pfmpe_ctx* c, int kid, Launch&& fn) {
   EventPair* ep = nullptr;
-  if (c->timing) {
+  if (c->timing_now) {
     if (c->ev_used == c->ev_pool.size()) {
       EventPair p{};
       p.kid = kid;
@@ -221,7 +223,7 @@ struct Seq {
                          c->record_counts ? c->d_counts : nullptr, c->d_out, seq, c->d_stamps);
     }));
     RET(wait_frame(c));
-    if (c->timing) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
+    if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;
   }
   static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs) {
@@ -486,7 +488,9 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       c->prune = value != 0;
       return PFMPE_OK;
     case PFMPE_OPT_TIMING:
-      c->timing = value != 0;
+      if (value < 0 || value > (1 << 20)) return fail(c, PFMPE_E_ARG, "set_option: timing period out of range");
+      c->timing = (int)value;
+      c->timing_frame = 0;
       return PFMPE_OK;
     case 99:  // undocumented: diagnostic kernel switches for timing experiments
       c->diag = (int)value;
@@ -574,8 +578,14 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     HIPCHK(c, hipMemcpyAsync(c->d_blobs, c->h_blobs, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice,
                              c->stream));
   }
-  RET(dispatch_step(c, in, blobs));
-  if (c->timing) RET(harvest_timing(c));
+  c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
+  const int rs = dispatch_step(c, in, blobs);
+  if (c->timing_now) {
+    c->timing_now = false;
+    if (rs == PFMPE_OK) RET(harvest_timing(c));
+    c->ev_used = 0;
+  }
+  RET(rs);
 
   const OutDev& o = *(const OutDev*)c->h_out;
   out->iters = o.iters;
@@ -598,6 +608,17 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   c->last_kept_slot = o.kept_slot;
   c->last_kept_iter = o.kept_iter;
   if (o.resampled) c->prior_idx = 1 - c->prior_idx;  // newPoseEstimation = resampled set (PE:681, 727)
+  return PFMPE_OK;
+}
+
+int pfmpe_step_batch(pfmpe_ctx* c, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out, int* done) {
+  if (!c) return PFMPE_E_ARG;
+  if (done) *done = 0;
+  if ((!in || !out) && n > 0) return fail(c, PFMPE_E_ARG, "step_batch: null in/out");
+  for (int f = 0; f < n; ++f) {
+    RET(pfmpe_step(c, in + f, out + f));
+    if (done) *done = f + 1;
+  }
   return PFMPE_OK;
 }
 

@@ -27,4 +27,10 @@ fi
 if [ "$what" = all ] || [ "$what" = prof ]; then
   step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-frames 0 --no-timing || exit 1
 fi
+if [ "$what" = all ] || [ "$what" = bench ]; then
+  step bench_pyloop 600 python bench.py --steps 200 --warmup 20 --cpu-frames 0 --python-loop || exit 1
+fi
+if [ "$what" = all ] || [ "$what" = pmc ]; then
+  step pmc 1000 bash scripts/pmc.sh c2_n100000 --steps 100 --warmup 10 || exit 1
+fi
 echo done

@@ -10,4 +10,4 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD S
   timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/pmc_$tag/p$i -o run -- python3 bench.py --cpu-frames 0 --no-timing "$@" > gpurun_out/pmc_${tag}_p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc_${tag}_p$i.log; exit $rc; fi
 done
-python3 scripts/pmc_summary.py gpurun_out/pmc_$tag
+python3 scripts/pmc_summary.py gpurun_out/pmc_$tag --json gpurun_out/pmc_$tag.json

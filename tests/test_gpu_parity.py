@@ -355,3 +355,28 @@ def test_frame_record_integrity_long_run():
         assert np.array_equal(out["pairs"], pairs), fr.index
         assert out["n_corr"] == len(pairs)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_step_batch_matches_step_loop():
+    """pfmpe_step_batch is the same frames through the same engine, looped in C."""
+    N = 5000
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 12)
+    res = []
+    for batch in (False, True):
+        eng = make_engine(N, st.markers, st.K, pf.STATE_F64, pf.RNG_PHILOX)
+        eng.set_prior(st.prior())
+        eng.stage_blob_bank([f.blobs for f in st.frames])
+        frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
+                                 dt=f.dt, seed=5 + f.index, frame_idx=f.index) for f in st.frames]
+        outs = eng.step_batch(frames) if batch else [eng.step(f) for f in frames]
+        res.append(([o.as_dict() if hasattr(o, "as_dict") else o for o in outs], eng.get_particles(1)))
+        eng.close()
+    (a, pa), (b, pb) = res
+    assert len(a) == len(b) == 12
+    for x, y in zip(a, b):
+        for k in ("iters", "kept_iter", "winner_idx", "accepted", "n_corr"):
+            assert x[k] == y[k]
+        assert np.array_equal(x["winner_pose"], y["winner_pose"])
+    assert np.array_equal(pa, pb)
