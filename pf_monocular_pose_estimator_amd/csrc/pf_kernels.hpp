@@ -205,10 +205,18 @@ __device__ __forceinline__ void compose(const T* A, const T* B, T* C) {
   }
 }
 
-// The motion model (PE:543-588) for particle n in PF iteration `iter`; P receives the 3x4 pose.
+// prior particle n (SoA planes), loaded ahead of use so the loads overlap other work
+template <typename T>
+__device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const T* __restrict__ prior, int n, T* A) {
+#pragma unroll
+  for (int q = 0; q < 12; ++q) A[q] = prior[(int64_t)q * fa.ld + n];
+}
+
+// The motion model (PE:543-588) for particle n in PF iteration `iter` from its prior pose A (loaded by
+// load_prior; unused for n < 2); P receives the 3x4 pose.
 template <typename T, int RNG>
-__device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc,
-                                              const T* __restrict__ prior, int n, int iter, T* P) {
+__device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* A_in, int n,
+                                          int iter, T* P) {
   if (n == 0) {  // current_pose_ (PE:547)
 #pragma unroll
     for (int q = 0; q < 12; ++q) P[q] = sc.cur[q];
@@ -221,7 +229,7 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const Lds
   }
   T A[12];
 #pragma unroll
-  for (int q = 0; q < 12; ++q) A[q] = prior[(int64_t)q * fa.ld + n];
+  for (int q = 0; q < 12; ++q) A[q] = A_in[q];
   if (fa.it > 1) {
     if (!fa.cam_identity) {  // camMoveInv * prior (PE:556-558)
       T X[12];
@@ -280,6 +288,14 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const Lds
   }
 }
 
+template <typename T, int RNG>
+__device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc,
+                                              const T* __restrict__ prior, int n, int iter, T* P) {
+  T A[12];
+  if (n >= 2) load_prior(fa, prior, n, A);
+  propagate<T, RNG>(fa, sc, A, n, iter, P);
+}
+
 // project2d (PE:1017-1034): p = (K34*T) * [X;1], u = p/p.z — full K, no distortion, no z>0 test
 template <typename T, int MAXM>
 __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* P, T* u,
@@ -316,7 +332,7 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
 
 // x -> bucket index (monotone in x; identical formula for table build and queries)
 template <typename T>
-__device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
+__host__ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
   const T f = (x - xmin) * inv_bw;
   if (!(f >= (T)0)) return 0;
   if (f >= (T)(kBuckets - 1)) return kBuckets - 1;
@@ -420,58 +436,77 @@ __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, c
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
-__device__ __forceinline__ double wave_incl_sum(double v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double t = __shfl_up(v, off, 64);
-    if (lane >= off) v = v + t;
-  }
-  return v;
+// All wave-level scans and reductions run on DPP lane moves (no LDS, no ds_bpermute): row_shr 1/2/4/8
+// builds the inclusive scan inside each 16-lane row, row_bcast:15 / row_bcast:31 carry row totals
+// across rows (GFX9-family DPP, kept by gfx950), so lane 63 ends with the wave total.  The pattern is
+// fixed, so a sum has ONE association everywhere it is evaluated (k_propagate_weigh and k_resample
+// must agree bit-for-bit).  Every lane of the wave must execute these (no divergent calls).
+enum : int {
+  kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118,
+  kDppWaveShr1 = 0x138, kDppBcast15 = 0x142, kDppBcast31 = 0x143
+};
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t src, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, CTRL, RM, 0xf, false);
 }
-__device__ __forceinline__ double wave_incl_max(double v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double t = __shfl_up(v, off, 64);
-    if (lane >= off && t > v) v = t;
-  }
-  return v;
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ int dpp(int src, int old) {
+  return (int)dpp_u32<CTRL, RM>((uint32_t)src, (uint32_t)old);
 }
-__device__ __forceinline__ double wave_incl_min(double v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double t = __shfl_up(v, off, 64);
-    if (lane >= off && t < v) v = t;
-  }
-  return v;
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ float dpp(float src, float old) {
+  return __uint_as_float(dpp_u32<CTRL, RM>(__float_as_uint(src), __float_as_uint(old)));
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double t = __shfl_xor(v, off, 64);
-    v = t > v ? t : v;
-  }
-  return v;
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ double dpp(double src, double old) {
+  const uint64_t s = (uint64_t)__double_as_longlong(src), o = (uint64_t)__double_as_longlong(old);
+  const uint32_t lo = dpp_u32<CTRL, RM>((uint32_t)s, (uint32_t)o);
+  const uint32_t hi = dpp_u32<CTRL, RM>((uint32_t)(s >> 32), (uint32_t)(o >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const double t = __shfl_xor(v, off, 64);
-    v = t < v ? t : v;
-  }
-  return v;
+// value of lane L in every lane (scalar result)
+__device__ __forceinline__ int lane_value(int x, int L) { return __builtin_amdgcn_readlane(x, L); }
+__device__ __forceinline__ float lane_value(float x, int L) {
+  return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(x), L));
 }
-__device__ __forceinline__ int wave_incl_sum_int(int v) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int t = __shfl_up(v, off, 64);
-    if (lane >= off) v += t;
-  }
-  return v;
+__device__ __forceinline__ double lane_value(double x, int L) {
+  const uint64_t v = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, L);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), L);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
+// lane i receives lane i-1's value, lane 0 receives `fill`
+template <typename V>
+__device__ __forceinline__ V wave_shr1(V x, V fill) {
+  return dpp<kDppWaveShr1>(x, fill);
+}
+
+struct OpSum {
+  __device__ double operator()(double a, double b) const { return a + b; }
+};
+struct OpMax {
+  __device__ double operator()(double a, double b) const { return b > a ? b : a; }
+};
+struct OpMin {
+  __device__ double operator()(double a, double b) const { return b < a ? b : a; }
+};
+// inclusive scan x_0 op ... op x_i; `id` is the identity of op
+template <typename V, typename Op>
+__device__ __forceinline__ V wave_scan(V x, V id, Op op) {
+  x = op(x, dpp<kDppRowShr1>(x, id));
+  x = op(x, dpp<kDppRowShr2>(x, id));
+  x = op(x, dpp<kDppRowShr4>(x, id));
+  x = op(x, dpp<kDppRowShr8>(x, id));
+  x = op(x, dpp<kDppBcast15, 0xa>(x, id));
+  x = op(x, dpp<kDppBcast31, 0xc>(x, id));
+  return x;
+}
+__device__ __forceinline__ double wave_incl_sum(double v) { return wave_scan(v, 0.0, OpSum()); }
+__device__ __forceinline__ double wave_incl_max(double v) { return wave_scan(v, -(double)INFINITY, OpMax()); }
+__device__ __forceinline__ double wave_incl_min(double v) { return wave_scan(v, (double)INFINITY, OpMin()); }
+__device__ __forceinline__ double wave_max(double v) { return lane_value(wave_incl_max(v), 63); }
+__device__ __forceinline__ double wave_min(double v) { return lane_value(wave_incl_min(v), 63); }
+
 // (value, index): larger value wins, lower index on ties
 template <typename V>
 __device__ __forceinline__ void cmb_max(V& v, int& i, V v2, int i2) {
@@ -487,15 +522,56 @@ __device__ __forceinline__ void cmb_min(V& v, int& i, V v2, int i2) {
     i = i2;
   }
 }
+// wave arg-reductions: the lexicographic (value, index) order is associative and commutative, so the
+// scan pattern reduces it exactly; the result is broadcast to every lane
+template <typename V, int CTRL, int RM = 0xf>
+__device__ __forceinline__ void argmax_step(V& v, int& i, V idv) {
+  const V v2 = dpp<CTRL, RM>(v, idv);
+  const int i2 = dpp<CTRL, RM>(i, 0x7fffffff);
+  cmb_max(v, i, v2, i2);
+}
+template <typename V, int CTRL, int RM = 0xf>
+__device__ __forceinline__ void argmin_step(V& v, int& i, V idv) {
+  const V v2 = dpp<CTRL, RM>(v, idv);
+  const int i2 = dpp<CTRL, RM>(i, 0x7fffffff);
+  cmb_min(v, i, v2, i2);
+}
 template <typename V>
 __device__ __forceinline__ void wave_argmax(V& v, int& i) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cmb_max(v, i, (V)__shfl_xor(v, off, 64), (int)__shfl_xor(i, off, 64));
+  const V id = -(V)INFINITY;
+  argmax_step<V, kDppRowShr1>(v, i, id);
+  argmax_step<V, kDppRowShr2>(v, i, id);
+  argmax_step<V, kDppRowShr4>(v, i, id);
+  argmax_step<V, kDppRowShr8>(v, i, id);
+  argmax_step<V, kDppBcast15, 0xa>(v, i, id);
+  argmax_step<V, kDppBcast31, 0xc>(v, i, id);
+  v = lane_value(v, 63);
+  i = lane_value(i, 63);
 }
 template <typename V>
 __device__ __forceinline__ void wave_argmin(V& v, int& i) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) cmb_min(v, i, (V)__shfl_xor(v, off, 64), (int)__shfl_xor(i, off, 64));
+  const V id = (V)INFINITY;
+  argmin_step<V, kDppRowShr1>(v, i, id);
+  argmin_step<V, kDppRowShr2>(v, i, id);
+  argmin_step<V, kDppRowShr4>(v, i, id);
+  argmin_step<V, kDppRowShr8>(v, i, id);
+  argmin_step<V, kDppBcast15, 0xa>(v, i, id);
+  argmin_step<V, kDppBcast31, 0xc>(v, i, id);
+  v = lane_value(v, 63);
+  i = lane_value(i, 63);
+}
+// int counts: "-infinity" is INT_MIN
+template <>
+__device__ __forceinline__ void wave_argmax<int>(int& v, int& i) {
+  const int id = (int)0x80000000;
+  argmax_step<int, kDppRowShr1>(v, i, id);
+  argmax_step<int, kDppRowShr2>(v, i, id);
+  argmax_step<int, kDppRowShr4>(v, i, id);
+  argmax_step<int, kDppRowShr8>(v, i, id);
+  argmax_step<int, kDppBcast15, 0xa>(v, i, id);
+  argmax_step<int, kDppBcast31, 0xc>(v, i, id);
+  v = lane_value(v, 63);
+  i = lane_value(i, 63);
 }
 
 // Deterministic block inclusive scan: pre_w = ((0 + t_0) + t_1) + ... over earlier waves' totals, then
@@ -532,14 +608,35 @@ __device__ __forceinline__ double target_r(const FrameArgsT<T>& fa, int iters, i
 // F(x) = #{k : r_k <= x}.  r_k is non-decreasing in k, so target k finds the first particle i whose
 // running-max cumulative weight R_i >= r_k (reference: first i with cumsum_i >= r_k, PE:674-679),
 // and particle i receives F(R_i) - F(R_{i-1}) copies.
+//
+// One evaluation decides F(x) almost always.  With xn = fl(x N), k = floor(xn), f = xn - k (exact):
+//   r_{k+1} >= fl((k+1)/N) >= (k+1)(1-2^-53)/N  and  x <= (k+f)/((1-2^-53)N), so r_{k+1} > x whenever
+//   1 - f > (k+1) 2^-52;
+//   r_{k-1} <= fl(k/N) <= k(1+2^-53)/N        and  x >= (k+f)/((1+2^-53)N), so r_{k-1} <= x whenever
+//   f > k 2^-51.
+// For N < 2^31 both bounds are below kEdge = 1e-6; inside that band (or for x N >= N) the neighbours
+// are scanned explicitly.
 template <typename T, int RNG>
 __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int iters, double x) {
+  constexpr double kEdge = 1e-6;
   const int64_t N = fa.N;
   if (!(x >= 0.0)) return 0;  // r_k >= 0; also -inf / NaN
-  const double fk = floor(x * (double)N);
-  int64_t k = fk < 0.0 ? 0 : (fk > (double)N ? N : (int64_t)fk);
-  while (k < N && target_r<T, RNG>(fa, iters, k) <= x) ++k;
-  while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
+  const double xn = x * (double)N;
+  const double fk = floor(xn);
+  if (!(fk < (double)N)) {  // x >= ~1: scan down from N
+    int64_t k = N;
+    while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
+    return k;
+  }
+  int64_t k = (int64_t)fk;
+  const double f = xn - fk;
+  if (target_r<T, RNG>(fa, iters, k) <= x) {
+    ++k;
+    if (1.0 - f <= kEdge)
+      while (k < N && target_r<T, RNG>(fa, iters, k) <= x) ++k;
+  } else if (f <= kEdge) {
+    while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
+  }
   return k;
 }
 
@@ -588,10 +685,13 @@ __device__ __forceinline__ bool arrive_last(uint32_t* counter, int count) {
 __device__ __forceinline__ bool wave_arrive_last(uint32_t* counter, int count) {
   int last = 0;
   if (lane_id() == 0) last = arrive_last(counter, count) ? 1 : 0;
-  return __shfl(last, 0, 64) != 0;
+  return lane_value(last, 0) != 0;
 }
 
-// Diagnostic stamps (fa.diag & 4 only): s_memrealtime (100 MHz)
+// Diagnostic stamps (fa.diag & 4 only): s_memrealtime (100 MHz).  0/4 first block start of K1/K2 (min),
+// 1/5 last block partial (max), 2-3 / 6-7 top wave start/end, 8 table built, 9 weights done, 10 K2 scan
+// done, 11 counts done, 12 scatter done, 13-18 finalize phases, 19 earliest table built (min).
+constexpr int kStamps = 32;
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ void stamp_min(uint64_t* st, int idx, uint64_t t) {
   if (st) atomicMin((unsigned long long*)(st + idx), (unsigned long long)t);
@@ -601,103 +701,90 @@ __device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
 }
 
 // ============================================================================== kernels
-// ---- per-block blob table in LDS (dynamic shared memory, sized by B): blobs grouped into x-buckets by a
-// counting sort.  Within a bucket the order is whatever the LDS atomics produce: candidate minima use
-// the explicit (distance, original index) order, so no result depends on it.
+// ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into kBuckets x-buckets,
+// built once per frame on the host (build_blob_table_host, O(B)) and copied whole into each block's
+// LDS by k_propagate_weigh.  Layout, every part 16-byte aligned:
+//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[kBuckets+1] | T bx[B] | T by[B] | int32 orig[B]
+// Within a bucket blobs keep increasing original index; candidate minima use the explicit
+// (distance, original index) order anyway, so no result depends on the bucket order.
+__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+template <typename T>
+struct BlobTable {
+  static constexpr size_t off_bstart() { return align16(4 * sizeof(T)); }
+  static constexpr size_t off_bx() { return off_bstart() + align16((kBuckets + 1) * 4); }
+  static constexpr size_t off_by(int B) { return off_bx() + align16((size_t)B * sizeof(T)); }
+  static constexpr size_t off_orig(int B) { return off_by(B) + align16((size_t)B * sizeof(T)); }
+  static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
+};
+
 template <typename T>
 struct LdsBlobs {
-  T* bx;
-  T* by;
-  int32_t* orig;
-  int32_t* bstart;  // kBuckets + 1
-  int32_t* fill;    // kBuckets
+  const T* bx;
+  const T* by;
+  const int32_t* orig;
+  const int32_t* bstart;  // kBuckets + 1
   T xmin, inv_bw, b0x, b0y;
 };
 
-__host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 template <typename T>
-__host__ __device__ constexpr size_t blob_lds_bytes(int B) {
-  return align16((size_t)B * sizeof(T)) * 2 + align16((size_t)B * 4) + align16((kBuckets + 1) * 4) +
-         align16(kBuckets * 4) + align16(2 * kWaves * sizeof(T));
+__host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* base, int B) {
+  LdsBlobs<T> t;
+  const T* hdr = (const T*)base;
+  t.xmin = hdr[0];
+  t.inv_bw = hdr[1];
+  t.b0x = hdr[2];
+  t.b0y = hdr[3];
+  t.bstart = (const int32_t*)(base + BlobTable<T>::off_bstart());
+  t.bx = (const T*)(base + BlobTable<T>::off_bx());
+  t.by = (const T*)(base + BlobTable<T>::off_by(B));
+  t.orig = (const int32_t*)(base + BlobTable<T>::off_orig(B));
+  return t;
 }
 
+// Host builder.  The bucket formula is bucket_of in T arithmetic (this TU: -ffp-contract=off), the
+// same expression the kernels evaluate for their query windows.
 template <typename T>
-__device__ LdsBlobs<T> build_blob_table(const FrameArgsT<T>& fa, const double* __restrict__ blobs,
-                                        unsigned char* smem) {
-  const int B = fa.B, tid = threadIdx.x;
-  LdsBlobs<T> t;
-  size_t off = 0;
-  t.bx = (T*)(smem + off);
-  off += align16((size_t)B * sizeof(T));
-  t.by = (T*)(smem + off);
-  off += align16((size_t)B * sizeof(T));
-  t.orig = (int32_t*)(smem + off);
-  off += align16((size_t)B * 4);
-  t.bstart = (int32_t*)(smem + off);
-  off += align16((kBuckets + 1) * 4);
-  t.fill = (int32_t*)(smem + off);
-  off += align16(kBuckets * 4);
-  T* red = (T*)(smem + off);
-
-  T lmin = inf_t<T>(), lmax = -inf_t<T>();
-  for (int i = tid; i < B; i += kBlock) {
+inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst) {
+  T xmin = (T)INFINITY, xmax = -(T)INFINITY;
+  for (int i = 0; i < B; ++i) {
     const T x = (T)blobs[2 * i];
-    lmin = x < lmin ? x : lmin;
-    lmax = x > lmax ? x : lmax;
+    xmin = x < xmin ? x : xmin;
+    xmax = x > xmax ? x : xmax;
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const T a = __shfl_xor(lmin, o, 64), b = __shfl_xor(lmax, o, 64);
-    lmin = a < lmin ? a : lmin;
-    lmax = b > lmax ? b : lmax;
-  }
-  if (lane_id() == 0) {
-    red[wave_id()] = lmin;
-    red[kWaves + wave_id()] = lmax;
-  }
-  for (int b = tid; b < kBuckets; b += kBlock) {
-    t.bstart[b] = 0;
-    t.fill[b] = 0;
-  }
-  __syncthreads();
-  T xmin = red[0], xmax = red[kWaves];
-#pragma unroll
-  for (int w = 1; w < kWaves; ++w) {
-    xmin = red[w] < xmin ? red[w] : xmin;
-    xmax = red[kWaves + w] > xmax ? red[kWaves + w] : xmax;
-  }
-  if (B == 0 || !(xmax - xmin < inf_t<T>())) {
+  if (B == 0 || !(xmax - xmin < (T)INFINITY)) {
     xmin = (T)0;
     xmax = (T)1;
   }
   T span = xmax - xmin;
   if (!(span > (T)0)) span = (T)1;
   const T inv_bw = (T)kBuckets / span;
-  for (int i = tid; i < B; i += kBlock) atomicAdd(&t.bstart[bucket_of((T)blobs[2 * i], xmin, inv_bw)], 1);
-  __syncthreads();
-  if (tid < 64) {  // exclusive scan of the 128 bucket counts, two per lane
-    const int c0 = t.bstart[2 * tid], c1 = t.bstart[2 * tid + 1];
-    const int incl = wave_incl_sum_int(c0 + c1);
-    const int excl = incl - c0 - c1;
-    t.bstart[2 * tid] = excl;
-    t.bstart[2 * tid + 1] = excl + c0;
-    if (tid == 63) t.bstart[kBuckets] = incl;
+  T* hdr = (T*)dst;
+  hdr[0] = xmin;
+  hdr[1] = inv_bw;
+  hdr[2] = B > 0 ? (T)blobs[0] : (T)0;
+  hdr[3] = B > 0 ? (T)blobs[1] : (T)0;
+  int32_t* bstart = (int32_t*)(dst + BlobTable<T>::off_bstart());
+  T* bx = (T*)(dst + BlobTable<T>::off_bx());
+  T* by = (T*)(dst + BlobTable<T>::off_by(B));
+  int32_t* orig = (int32_t*)(dst + BlobTable<T>::off_orig(B));
+  int32_t cnt[kBuckets + 1] = {0};
+  for (int i = 0; i < B; ++i) ++cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw) + 1];
+  for (int b = 0; b < kBuckets; ++b) cnt[b + 1] += cnt[b];
+  for (int b = 0; b <= kBuckets; ++b) bstart[b] = cnt[b];
+  for (int i = 0; i < B; ++i) {
+    const int pos = cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw)]++;
+    bx[pos] = (T)blobs[2 * i];
+    by[pos] = (T)blobs[2 * i + 1];
+    orig[pos] = i;
   }
-  __syncthreads();
-  for (int i = tid; i < B; i += kBlock) {
-    const T x = (T)blobs[2 * i], y = (T)blobs[2 * i + 1];
-    const int b = bucket_of(x, xmin, inv_bw);
-    const int pos = t.bstart[b] + atomicAdd(&t.fill[b], 1);
-    t.bx[pos] = x;
-    t.by[pos] = y;
-    t.orig[pos] = i;
-  }
-  t.xmin = xmin;
-  t.inv_bw = inv_bw;
-  t.b0x = B > 0 ? (T)blobs[0] : (T)0;
-  t.b0y = B > 0 ? (T)blobs[1] : (T)0;
-  __syncthreads();
-  return t;
+}
+
+// block-wide copy of the table into LDS (16-byte words); callers barrier before use
+__device__ __forceinline__ void copy_table(const unsigned char* __restrict__ src, unsigned char* dst, size_t bytes) {
+  const uint4* s4 = (const uint4*)src;
+  uint4* d4 = (uint4*)dst;
+  const int n4 = (int)(bytes / 16);
+  for (int i = threadIdx.x; i < n4; i += kBlock) d4[i] = s4[i];
 }
 
 // ---- group wave of k_propagate_weigh: lanes <-> the <= 64 blocks of group g
@@ -720,22 +807,21 @@ __device__ void propagate_group(int nblk, int g, const BlockPart* __restrict__ p
     amin = hi32(ai);
   }
   const double incl = wave_incl_sum(sum);
-  const double prev = __shfl_up(incl, 1, 64);
-  const double E = lane == 0 ? 0.0 : prev;  // exclusive prefix = previous lane's inclusive value
+  const double E = wave_shr1(incl, 0.0);  // exclusive prefix = previous lane's inclusive value
   const double zmax = vb ? E + maxrel : -INFINITY;
   const double zmin = vb ? E + minrel : INFINITY;
   const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
-  const double zp_max = __shfl_up(zi_max, 1, 64), zp_min = __shfl_up(zi_min, 1, 64);
+  const double zp_max = wave_shr1(zi_max, -(double)INFINITY), zp_min = wave_shr1(zi_min, (double)INFINITY);
   if (vb) {
     BlockScan s;
     s.E = E;
-    s.zin_max = lane == 0 ? -INFINITY : zp_max;
-    s.zin_min = lane == 0 ? INFINITY : zp_min;
+    s.zin_max = zp_max;
+    s.zin_min = zp_min;
     s.pad = 0.0;
     bscan[b] = s;
   }
-  const double gsum = __shfl(incl, 63, 64);
-  const double gzmax = __shfl(zi_max, 63, 64), gzmin = __shfl(zi_min, 63, 64);
+  const double gsum = lane_value(incl, 63);
+  const double gzmax = lane_value(zi_max, 63), gzmin = lane_value(zi_min, 63);
   wave_argmax(maxw, amax);
   wave_argmin(minw, amin);
   if (lane == 0) {
@@ -792,10 +878,10 @@ __device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __r
     const int g = base + lane;
     const double s = g < ngrp ? ld_wt_d(&KG[g].sum) : 0.0;
     const double incl = wave_incl_sum(s);
-    const double prev = __shfl_up(incl, 1, 64);
+    const double prev = wave_shr1(incl, 0.0);
     const double G = lane == 0 ? carry : carry + prev;
     if (g < ngrp) gscan[g].G = G;
-    carry = carry + __shfl(incl, 63, 64);
+    carry = carry + lane_value(incl, 63);
   }
   const double S = carry;
   // running max of c at each group start: Gin_g = max over earlier groups of fl(fl(G + z)/S)
@@ -809,11 +895,10 @@ __device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __r
         cm = (gscan[g].G + z) / S;
       }
       const double im = wave_incl_max(cm);
-      const double im_prev = __shfl_up(im, 1, 64);  // every lane executes the shuffle (no divergence)
-      double ex = lane == 0 ? -INFINITY : im_prev;
+      double ex = wave_shr1(im, -(double)INFINITY);
       ex = ex > run ? ex : run;
       if (g < ngrp) gscan[g].Gin = ex;
-      const double tm = __shfl(im, 63, 64);
+      const double tm = lane_value(im, 63);
       run = tm > run ? tm : run;
     }
   }
@@ -847,7 +932,7 @@ __device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __r
 // ---- launch 1: motion + projection + likelihood, one particle per thread
 template <typename T, int RNG, int MAXM, bool PRUNE>
 __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
-    const FrameArgsT<T> fa, const double* __restrict__ blobs, const T* __restrict__ prior, T* __restrict__ w0,
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ w0,
     T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
     BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
     GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
@@ -858,18 +943,29 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   __shared__ int s_ix[kWaves], s_in[kWaves];
 
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  // table loads first: vmcnt retires in order, so the LDS copy then waits only for them while the
+  // prior loads stay in flight across the barrier
+  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
   const Ctrl c0 = *ctrl;
   if (c0.done) return;  // the exit rule already fired (uniform)
   const int slot = c0.cur_slot;
-  stage_consts(fa, sc);  // made visible by the barriers inside build_blob_table
-  const LdsBlobs<T> tb = build_blob_table<T>(fa, blobs, smem);
+  stage_consts(fa, sc);
+  __syncthreads();  // table + constants visible
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  if (stamps && threadIdx.x == 0) {
+    const uint64_t t = rt_now();
+    stamp_max(stamps, 8, t);
+    stamp_min(stamps, 19, t);
+  }
 
-  const int n = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = n < fa.N;
   T w = (T)0;
   if (valid) {
     T P[12], u[MAXM], v[MAXM];
-    make_particle<T, RNG>(fa, sc, prior, n, iter, P);
+    propagate<T, RNG>(fa, sc, A, n, iter, P);
     project_markers<T, MAXM>(fa, sc, P, u, v);
     if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
       T m[MAXM];
@@ -879,6 +975,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     }
     (slot ? w1 : w0)[n] = w;
   }
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
   // wave partials: scan total, extrema of the wave-inclusive prefix, max/argmax, min/argmin
   const double wd = valid ? (double)w : 0.0;
   const double wi = wave_incl_sum(wd);
@@ -929,7 +1026,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     if (stamps) stamp_max(stamps, 1, rt_now());
     last = arrive_last(gcount + g, gsize) ? 1 : 0;
   }
-  if (!__shfl(last, 0, 64)) return;
+  if (!lane_value(last, 0)) return;
   propagate_group(fa.nblk, g, slot ? part1 : part0, slot ? bscan1 : bscan0, slot ? gpart1 : gpart0);
   if (!wave_arrive_last(tcount, fa.ngrp)) return;
   if (stamps && lane == 0) stamps[2] = rt_now();
@@ -938,45 +1035,89 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
 }
 
 // ---- winner + frame record (one wave).  Writes into pinned host memory, then resets the control
-// record for the next frame.
+// record for the next frame.  Lanes 0-31 regenerate the most likely particle and lanes 32-63 the winner
+// in one pass; the winner's column minima run over blobs held one per lane (loaded once).
 template <typename T, int RNG, int MAXM>
 __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
-                               const double* __restrict__ blobs, const T* __restrict__ prior, int winner,
-                               OutDev& rec, OutDev* __restrict__ out, int32_t tag) {
+                               const unsigned char* __restrict__ table, const T* __restrict__ prior, int winner,
+                               OutDev& rec, OutDev* __restrict__ out, int32_t tag, uint64_t* __restrict__ stamps) {
   const int lane = lane_id();
+  const int B = fa.B;
+  const LdsBlobs<T> tb = view_table<T>(table, B);  // global memory here
+  // table entries of this lane (chunk 0 covers B <= 64; larger B loops below)
+  T bx0 = (T)0, by0 = (T)0;
+  int o0 = 0x7fffffff;
+  if (lane < B) {
+    bx0 = tb.bx[lane];
+    by0 = tb.by[lane];
+    o0 = tb.orig[lane];
+  }
+  const int wsel = c.accepted ? winner : c.most_likely_idx;
+  T Q[12];
+  make_particle<T, RNG>(fa, sc, prior, lane < 32 ? c.most_likely_idx : wsel, c.kept_iter, Q);
   T Pm[12], P[12];
-  make_particle<T, RNG>(fa, sc, prior, c.most_likely_idx, c.kept_iter, Pm);
+#pragma unroll
+  for (int q = 0; q < 12; ++q) {
+    Pm[q] = lane_value(Q[q], 0);
+    P[q] = lane_value(Q[q], 32);
+  }
+  if (stamps && lane == 0) stamps[13] = stamps[14] = rt_now();
+  if (lane < 2 * kMaxMarkers) rec.corr[lane] = 0u;
   int np = 0;
-  uint32_t pairs[2 * MAXM];
   if (c.accepted) {
-    make_particle<T, RNG>(fa, sc, prior, winner, c.kept_iter, P);
     T u[MAXM], v[MAXM], m[MAXM];
     int r[MAXM];
     project_markers<T, MAXM>(fa, sc, P, u, v);
-    // column minima of the winner, blobs spread over the lanes (first index on ties)
+    T best[MAXM];
+    int arg[MAXM];
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
-      T best = inf_t<T>();
-      int arg = 0x7fffffff;
-      if (j < fa.M)
-        for (int i = lane; i < fa.B; i += 64) {
-          const T dx = (T)blobs[2 * i] - u[j];
-          const T dy = (T)blobs[2 * i + 1] - v[j];
+      best[j] = inf_t<T>();
+      arg[j] = 0x7fffffff;
+    }
+    // (distance, original index) order, as column_minima
+    for (int base = 0; base < B; base += 64) {
+      const int i = base + lane;
+      T bx = bx0, by = by0;
+      int o = o0;
+      if (base > 0 && i < B) {
+        bx = tb.bx[i];
+        by = tb.by[i];
+        o = tb.orig[i];
+      }
+      if (i < B) {
+#pragma unroll
+        for (int j = 0; j < MAXM; ++j) {
+          const T dx = bx - u[j];
+          const T dy = by - v[j];
           const T d = fmadd(dx, dx, dy * dy);
-          if (d < best) {
-            best = d;
-            arg = i;
+          if (d < best[j] || (d == best[j] && o < arg[j])) {
+            best[j] = d;
+            arg[j] = o;
           }
         }
-      wave_argmin(best, arg);
-      m[j] = best;
-      r[j] = arg == 0x7fffffff ? 0 : arg;
+      }
     }
-    if (fa.B > 0 && !nan_at_origin((T)blobs[0], (T)blobs[1], u[0], v[0]))
-      score_minima<T, MAXM, true>(fa, m, r, pairs, &np);
-  } else {
 #pragma unroll
-    for (int q = 0; q < 12; ++q) P[q] = Pm[q];
+    for (int j = 0; j < MAXM; ++j) {
+      if (j < fa.M) wave_argmin(best[j], arg[j]);  // uniform branch
+      m[j] = best[j];
+      r[j] = arg[j] == 0x7fffffff ? 0 : arg[j];
+    }
+    if (stamps && lane == 0) stamps[15] = rt_now();
+    if (lane == 0 && B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0]))
+      score_minima<T, MAXM, true>(fa, m, r, rec.corr, &np);  // pairs straight into the LDS record
+    if (stamps && lane == 0) stamps[16] = rt_now();
+  }
+  if (lane < 12) {  // lane q writes pose word q (selects, no dynamic register indexing)
+    T pm = Pm[0], pw = P[0];
+#pragma unroll
+    for (int q = 1; q < 12; ++q) {
+      pm = lane == q ? Pm[q] : pm;
+      pw = lane == q ? P[q] : pw;
+    }
+    rec.most_likely_pose[lane] = (double)pm;
+    rec.winner_pose[lane] = (double)pw;
   }
   if (lane == 0) {
     rec.kept_slot = c.kept_slot;
@@ -989,15 +1130,8 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
     rec.flag_fail = c.accepted ? 1 : 4;
     rec.highest_prob = c.has_best ? c.best_max : 0.0;
     rec.prob_sum = c.S;
-#pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      rec.most_likely_pose[q] = (double)Pm[q];
-      rec.winner_pose[q] = (double)P[q];
-    }
-#pragma unroll
-    for (int q = 0; q < 2 * MAXM; ++q) rec.corr[q] = q < 2 * np ? pairs[q] : 0u;
-    for (int q = 2 * MAXM; q < 2 * kMaxMarkers; ++q) rec.corr[q] = 0u;
     rec.n_corr = np;
+    if (stamps) stamps[17] = rt_now();
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1007,6 +1141,7 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
   if (lane == kWords) st_sys32(&out->kept_slot, (uint32_t)rec.kept_slot);
   if (lane != 0) return;
   publish_tag(&out->tag, tag);
+  if (stamps) stamps[18] = rt_now();
   // the next frame starts from the all-zero control record
   Ctrl z;
   z.best_max = 0.0;
@@ -1022,7 +1157,7 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
 // particles; the last group's wave picks the winner and writes the frame record
 template <typename T, int RNG, int MAXM>
 __global__ __launch_bounds__(kBlock) void k_resample(
-    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const double* __restrict__ blobs, const T* __restrict__ prior,
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const T* __restrict__ prior,
     T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
@@ -1035,33 +1170,42 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   __shared__ int s_c[kWaves], s_ci[kWaves];
 
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
-  const Ctrl c = *ctrl;
-  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
-    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
-    return;
-  }
-  stage_consts(fa, sc);
-  __syncthreads();
-  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
-    if (blockIdx.x == 0 && threadIdx.x < 64)
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, blobs, prior, -1, rec, out, 2 * seq + 1);
-    return;
-  }
-  const int slot = c.kept_slot, kiter = c.kept_iter, iters = c.iters;
-  const double S = c.S;
-  const int64_t Kt = c.K_total;
   const int N = fa.N;
   const int blk = blockIdx.x, lane = lane_id(), wv = wave_id();
   const int g = blk / kGroup;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < N;
-  const T* W = slot ? w1 : w0;
-  const BlockScan bs = (slot ? bscan1 : bscan0)[blk];
+  // Everything that does not depend on the control record is requested first (both weight slots: the
+  // kept one is known only from ctrl), so the loads overlap the ctrl read.
+  T wt0 = (T)0, wt1 = (T)0;
+  if (valid) {
+    wt0 = w0[n];
+    wt1 = w1[n];
+  }
+  const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
   const GroupScan gs = gscan[g];
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  const Ctrl c = *ctrl;
+  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
+    return;
+  }
+  stage_consts(fa, sc);  // visible after block_incl_sum's barrier (finalize below: same wave)
+  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
+    if (blockIdx.x == 0 && threadIdx.x < 64)
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
+    return;
+  }
+  const int slot = c.kept_slot, kiter = c.kept_iter, iters = c.iters;
+  const double S = c.S;
+  const int64_t Kt = c.K_total;
+  const BlockScan bs = slot ? bsb : bsa;
 
-  const double wd = valid ? (double)W[n] : 0.0;
+  const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   double incl;
   block_incl_sum(wd, incl, s_sum);
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 10, rt_now());
   const double cn = (gs.G + (bs.E + incl)) / S;
   // running max of c seeded by the exact running max at the block start:
   // max(Gin_g, fl(fl(G_g + zin_b)/S)); zin_b = -inf (S > 0) / +inf (S < 0) for a group's first block
@@ -1081,9 +1225,10 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   const int hi = valid ? (int)count_targets<T, RNG>(fa, iters, R) : N;
   if (lane == 63) s_hi[wv] = hi;
   __syncthreads();
-  int lo = __shfl_up(hi, 1, 64);
+  int lo = wave_shr1(hi, 0);
   if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : s_hi[wv - 1];
   const int cntn = valid ? hi - lo : 0;
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 11, rt_now());
   if (counts && valid) counts[n] = (uint32_t)cntn;
 
   // write range [a, e): targets past K_total find nothing and copy the last found particle (the
@@ -1118,11 +1263,11 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   T P[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) P[q] = (T)0;
-  if (e > a) make_particle<T, RNG>(fa, sc, prior, n, kiter, P);
+  if (e > a) propagate<T, RNG>(fa, sc, A, n, kiter, P);
 
   // wave-cooperative scatter: the wave's lanes own consecutive slot ranges [a, e)
-  const int wa = __shfl(a, 0, 64);
-  const int we = __shfl(e, 63, 64);
+  const int wa = lane_value(a, 0);
+  const int we = lane_value(e, 63);
   for (int base = wa; base < we; base += 64) {
     const int k = base + lane;
     int l = 0;
@@ -1140,6 +1285,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     }
   }
 
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 12, rt_now());
   __syncthreads();
   if (wv != 0) return;
   int last = 0;
@@ -1150,7 +1296,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     if (stamps) stamp_max(stamps, 5, rt_now());
     last = arrive_last(gcount + g, min(kGroup, fa.nblk - g * kGroup)) ? 1 : 0;
   }
-  if (!__shfl(last, 0, 64)) return;
+  if (!lane_value(last, 0)) return;
   {  // group: max count over its blocks
     const int b = g * kGroup + lane;
     int bv = -1, bi = 0x7fffffff;
@@ -1171,7 +1317,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     cmb_max(bv, bi, lo32(cp), hi32(cp));
   }
   wave_argmax(bv, bi);
-  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, blobs, prior, bi, rec, out, 2 * seq + 1);
+  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, bi, rec, out, 2 * seq + 1, stamps);
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 

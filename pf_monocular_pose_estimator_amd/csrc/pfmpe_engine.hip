@@ -54,10 +54,11 @@ struct pfmpe_ctx {
   OutDev* h_out = nullptr;       // pinned host memory, written by the final wave
   OutDev* d_out = nullptr;       // its device address
   int32_t seq = 0;               // frame-record sequence number (publication tag = 2 * seq + finished)
-  double* d_blobs = nullptr;
-  double* h_blobs = nullptr;     // pinned staging
-  double* d_bank = nullptr;
-  std::vector<int32_t> bank_off;
+  unsigned char* d_table = nullptr;  // this frame's blob table (BlobTable<T> layout)
+  unsigned char* h_table = nullptr;  // pinned staging
+  unsigned char* d_bank = nullptr;   // staged tables of a whole stream, back to back
+  std::vector<size_t> bank_off;      // byte offset of frame f's table
+  std::vector<int32_t> bank_B;
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
@@ -191,25 +192,25 @@ template <> FrameArgsT<double>& last_args<double>(pfmpe_ctx* c) { return c->last
 
 template <typename T, int RNG, int MAXM>
 struct Seq {
-  static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs, int iter) {
+  static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, int iter) {
     const T* prior = (const T*)c->d_state[c->prior_idx];
-    const size_t lds = blob_lds_bytes<T>(fa.B);
+    const size_t lds = BlobTable<T>::bytes(fa.B);
     uint32_t* gcount = c->d_counters;
     uint32_t* tcount = c->d_counters + c->max_grp;
     return launch(c, PFMPE_K_PROPAGATE, [&] {
       if (c->prune)
         hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
-                           blobs, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
+                           table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
                            c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
                            c->d_stamps);
       else
         hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
-                           blobs, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
+                           table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
                            c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
                            c->d_stamps);
     });
   }
-  static int finish(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs) {
+  static int finish(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
     const T* prior = (const T*)c->d_state[c->prior_idx];
     T* post = (T*)c->d_state[1 - c->prior_idx];
     uint32_t* gcount = c->d_counters + c->max_grp + 1;
@@ -217,7 +218,7 @@ struct Seq {
     c->seq = (c->seq + 1) & 0x3fffffff;
     const int32_t seq = c->seq;
     RET(launch(c, PFMPE_K_RESAMPLE, [&] {
-      hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, blobs,
+      hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_out, seq, c->d_stamps);
@@ -226,18 +227,18 @@ struct Seq {
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;
   }
-  static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const double* blobs) {
+  static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
     const int iter_cap = fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter);
     int iter = 0;
-    RET(iterate(c, fa, blobs, iter++));
-    RET(finish(c, fa, blobs));
+    RET(iterate(c, fa, table, iter++));
+    RET(finish(c, fa, table));
     // Rare path: the exit rule did not fire on iteration 0.  Later iterations are queued in growing
     // batches; launches past the exit are no-ops (they read ctrl->done).
     int batch = 1;
     while (!frame_done(c)) {
       if (iter >= iter_cap) return fail(c, PFMPE_E_STATE, "PF iteration loop did not terminate");
-      for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, blobs, iter++));
-      RET(finish(c, fa, blobs));
+      for (int b = 0; b < batch && iter < iter_cap; ++b) RET(iterate(c, fa, table, iter++));
+      RET(finish(c, fa, table));
       batch = std::min(batch * 2, 16);
     }
     last_args<T>(c) = fa;
@@ -256,17 +257,17 @@ template <typename T>
 FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
 
 template <typename T, int RNG>
-int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const double* blobs) {
+int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
   const FrameArgsT<T> fa = build_args<T>(c, in);
-  if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, blobs);
-  return Seq<T, RNG, 16>::step(c, fa, blobs);
+  if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, table);
+  return Seq<T, RNG, 16>::step(c, fa, table);
 }
 
-int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const double* blobs) {
+int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
   const bool f64 = c->state_dtype == PFMPE_STATE_F64;
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
-  if (f64) return ref ? dispatch_m<double, kRngReference>(c, in, blobs) : dispatch_m<double, kRngPhilox>(c, in, blobs);
-  return ref ? dispatch_m<float, kRngReference>(c, in, blobs) : dispatch_m<float, kRngPhilox>(c, in, blobs);
+  if (f64) return ref ? dispatch_m<double, kRngReference>(c, in, table) : dispatch_m<double, kRngPhilox>(c, in, table);
+  return ref ? dispatch_m<float, kRngReference>(c, in, table) : dispatch_m<float, kRngPhilox>(c, in, table);
 }
 
 int dispatch_regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
@@ -345,17 +346,27 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   return fa;
 }
 
+size_t table_bytes(const pfmpe_ctx* c, int B) {
+  return c->state_dtype == PFMPE_STATE_F64 ? BlobTable<double>::bytes(B) : BlobTable<float>::bytes(B);
+}
+void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* dst) {
+  if (c->state_dtype == PFMPE_STATE_F64)
+    build_blob_table_host<double>(blobs, B, dst);
+  else
+    build_blob_table_host<float>(blobs, B, dst);
+}
+
 size_t counters_bytes(const pfmpe_ctx* c) { return (size_t)(2 * c->max_grp + 2) * sizeof(uint32_t); }
 
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
-                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_blobs, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (c->h_out) (void)hipHostFree(c->h_out);
-  if (c->h_blobs) (void)hipHostFree(c->h_blobs);
+  if (c->h_table) (void)hipHostFree(c->h_table);
   for (auto& e : c->ev_pool) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -427,9 +438,8 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
   ok &= hipHostMalloc((void**)&c->h_out, sizeof(OutDev), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
   ok = ok && hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_blobs, (size_t)kMaxBlobs * 2 * sizeof(double)) == hipSuccess;
-  ok &= hipHostMalloc((void**)&c->h_blobs, (size_t)kMaxBlobs * 2 * sizeof(double), hipHostMallocDefault) ==
-        hipSuccess;
+  ok &= hipMalloc((void**)&c->d_table, table_bytes(c, kMaxBlobs)) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_table, table_bytes(c, kMaxBlobs), hipHostMallocDefault) == hipSuccess;
   if (!ok) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_ctrl, 0, sizeof(Ctrl)) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_counters, 0, counters_bytes(c)) != hipSuccess) return bad(PFMPE_E_HIP);
@@ -496,7 +506,7 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       c->diag = (int)value;
       if ((c->diag & 4) && !c->d_stamps) {
         RET(set_device(c));
-        HIPCHK(c, hipMalloc((void**)&c->d_stamps, 8 * sizeof(uint64_t)));
+        HIPCHK(c, hipMalloc((void**)&c->d_stamps, kStamps * sizeof(uint64_t)));
       }
       return PFMPE_OK;
     default:
@@ -546,11 +556,17 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
     HIPCHK(c, hipFree(c->d_bank));
     c->d_bank = nullptr;
   }
-  const size_t rows = (size_t)std::max(1, offsets[nframes]);
-  HIPCHK(c, hipMalloc((void**)&c->d_bank, rows * 2 * sizeof(double)));
-  if (offsets[nframes] > 0)
-    HIPCHK(c, hipMemcpy(c->d_bank, blobs, (size_t)offsets[nframes] * 2 * sizeof(double), hipMemcpyHostToDevice));
-  c->bank_off.assign(offsets, offsets + nframes + 1);
+  c->bank_off.assign(nframes + 1, 0);
+  c->bank_B.assign(nframes, 0);
+  for (int f = 0; f < nframes; ++f) {
+    c->bank_B[f] = offsets[f + 1] - offsets[f];
+    c->bank_off[f + 1] = c->bank_off[f] + table_bytes(c, c->bank_B[f]);
+  }
+  std::vector<unsigned char> host(c->bank_off[nframes]);
+  for (int f = 0; f < nframes; ++f)
+    build_table(c, blobs + 2 * (size_t)offsets[f], c->bank_B[f], host.data() + c->bank_off[f]);
+  HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
+  HIPCHK(c, hipMemcpy(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice));
   return PFMPE_OK;
 }
 
@@ -563,23 +579,21 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   if (in->it_since_init >= 2 && !(in->dt != 0.0))
     return fail(c, PFMPE_E_ARG, "step: dt must be non-zero in steady state");
   RET(set_device(c));
-  const double* blobs = c->d_blobs;
-  int B = in->B;
+  const unsigned char* table = c->d_table;
+  const int B = in->B;
   if (in->bank_frame >= 0) {
-    if (!c->d_bank || in->bank_frame + 1 >= (int)c->bank_off.size())
+    if (!c->d_bank || in->bank_frame >= (int)c->bank_B.size())
       return fail(c, PFMPE_E_ARG, "step: bank_frame out of range");
-    const int off = c->bank_off[in->bank_frame];
-    B = c->bank_off[in->bank_frame + 1] - off;
-    if (B != in->B) return fail(c, PFMPE_E_ARG, "step: B does not match the staged bank frame");
-    blobs = c->d_bank + 2 * (size_t)off;
-  } else if (B > 0) {
-    if (!in->blobs) return fail(c, PFMPE_E_ARG, "step: null blobs");
-    std::memcpy(c->h_blobs, in->blobs, (size_t)B * 2 * sizeof(double));
-    HIPCHK(c, hipMemcpyAsync(c->d_blobs, c->h_blobs, (size_t)B * 2 * sizeof(double), hipMemcpyHostToDevice,
-                             c->stream));
+    if (c->bank_B[in->bank_frame] != B) return fail(c, PFMPE_E_ARG, "step: B does not match the staged bank frame");
+    table = c->d_bank + c->bank_off[in->bank_frame];
+  } else {
+    if (B > 0 && !in->blobs) return fail(c, PFMPE_E_ARG, "step: null blobs");
+    // the x-bucketed table is built here, O(B), and travels in the same copy the blobs would
+    build_table(c, in->blobs, B, c->h_table);
+    HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, table_bytes(c, B), hipMemcpyHostToDevice, c->stream));
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
-  const int rs = dispatch_step(c, in, blobs);
+  const int rs = dispatch_step(c, in, table);
   if (c->timing_now) {
     c->timing_now = false;
     if (rs == PFMPE_OK) RET(harvest_timing(c));
@@ -675,17 +689,18 @@ int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
   return PFMPE_OK;
 }
 
-// Undocumented diagnostic: reset (out == NULL) or read the 8 stamps of the last frame (diag & 4).
+// Undocumented diagnostic: reset (out == NULL) or read the kStamps stamps of the last frame (diag & 4).
 int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
   if (!c || !c->d_stamps) return PFMPE_E_STATE;
   RET(set_device(c));
   if (!out) {
-    uint64_t init[8] = {~0ull, 0, 0, 0, ~0ull, 0, 0, 0};
+    uint64_t init[kStamps] = {0};
+    init[0] = init[4] = init[19] = ~0ull;  // min-stamps
     HIPCHK(c, hipMemcpy(c->d_stamps, init, sizeof(init), hipMemcpyHostToDevice));
     return PFMPE_OK;
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  HIPCHK(c, hipMemcpy(out, c->d_stamps, 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(out, c->d_stamps, kStamps * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return PFMPE_OK;
 }
 

@@ -14,10 +14,15 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
     for fr in st.frames:
         lib.pfmpe_debug_stamps(eng.ctx, None)
         eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt, seed=3, frame_idx=fr.index))
-        s = (C.c_uint64 * 8)(); lib.pfmpe_debug_stamps(eng.ctx, s)
+        s = (C.c_uint64 * 32)(); lib.pfmpe_debug_stamps(eng.ctx, s)
         t = np.array(list(s), dtype=np.float64)
         t0 = t[0]
-        rows.append([(t[i] - t0) / 100.0 for i in range(8)])  # us (100 MHz)
+        rows.append([(t[i] - t0) / 100.0 if t[i] else float('nan') for i in range(32)])  # us (100 MHz)
     r = np.median(np.array(rows[5:]), axis=0)
     print(f"N={N}: K1 start 0 | last arrival {r[1]:.2f} | reduce {r[2]:.2f}->{r[3]:.2f} ({r[3]-r[2]:.2f}) || K2 start {r[4]:.2f} | last arrival {r[5]:.2f} | final {r[6]:.2f}->{r[7]:.2f} ({r[7]-r[6]:.2f})  [us]")
+    names = {8: "K1 table built (last)", 19: "K1 table built (first)", 9: "K1 weights (last)", 10: "K2 scan (last)",
+             11: "K2 counts (last)", 12: "K2 scatter (last)", 13: "fin Pm", 14: "fin P", 15: "fin minima",
+             16: "fin score", 17: "fin record", 18: "fin published"}
+    for i in sorted(names, key=lambda i: r[i]):
+        print(f"    {names[i]:24s} {r[i]:8.2f}")
     eng.close()

@@ -1,0 +1,9 @@
+#!/bin/bash
+# quick GPU loop: parity tests, phase stamps, bench (each step time-limited; stop on the first failure)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -15 gpurun_out/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python scripts/diag_stamps.py ${STAMP_N:-100000 1000000} > gpurun_out/stamps.log 2>&1 || { cat gpurun_out/stamps.log; exit 1; }
+cat gpurun_out/stamps.log
+timeout -k 10 300 python bench.py --cpu-frames 0 > gpurun_out/bench.log 2>&1 || { tail gpurun_out/bench.log; exit 1; }
+cat gpurun_out/bench.log
