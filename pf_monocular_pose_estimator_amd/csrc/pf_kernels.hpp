@@ -388,45 +388,74 @@ __device__ __forceinline__ bool nan_at_origin(T b0x, T b0y, T u0, T v0) {
   return d != d;
 }
 
+// Extraction order = ascending (m_j, j): column minima are never NaN (they start at +inf and a NaN
+// distance never compares smaller), so a sorting network on the (m_j, j) keys yields exactly the pair
+// sequence of the reference's repeated minCoeff.  Batcher's odd-even merge sort, fully unrolled
+// (MAXM = 8: 19 compare-exchanges); markers j >= M sort last with key +inf and lie beyond L anyway.
+template <typename T>
+__device__ __forceinline__ void cas_key(T& ma, int& ja, int& ra, T& mb, int& jb, int& rb) {
+  const bool sw = mb < ma || (mb == ma && jb < ja);
+  const T m0 = sw ? mb : ma, m1 = sw ? ma : mb;
+  const int j0 = sw ? jb : ja, j1 = sw ? ja : jb;
+  const int r0 = sw ? rb : ra, r1 = sw ? ra : rb;
+  ma = m0; mb = m1; ja = j0; jb = j1; ra = r0; rb = r1;
+}
+template <typename T, int MAXM>
+__device__ __forceinline__ void sort_minima(T* km, int* kj, int* kr) {
+#pragma unroll
+  for (int p = 1; p < MAXM; p <<= 1)
+#pragma unroll
+    for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+      for (int j = k % p; j + k < MAXM; j += 2 * k)
+#pragma unroll
+        for (int i = 0; i < k; ++i)
+          if (i + j + k < MAXM && (i + j) / (2 * p) == (i + j + k) / (2 * p))
+            cas_key(km[i + j], kj[i + j], kr[i + j], km[i + j + k], kj[i + j + k], kr[i + j + k]);
+}
+
 template <typename T, int MAXM, bool PAIRS>
 __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, const int* r, uint32_t* pairs,
                                           int* npairs) {
   const int B = fa.B, M = fa.M;
   const int L = B < M ? B : M;
   const T tol = fa.tol, tol_pf = fa.tol_pf, Mt = (T)M;
+  T km[MAXM];
+  int kj[MAXM], kr[MAXM];
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    km[j] = j < M ? m[j] : inf_t<T>();
+    kj[j] = j;
+    kr[j] = r[j];
+  }
+  sort_minima<T, MAXM>(km, kj, kr);
   T Pr = (T)0;
   int s = 1;
-  uint32_t taken = 0u;
+  bool live = true;
   if (PAIRS) *npairs = 0;
-  for (int k = 0; k < L; ++k) {
-    T best = (T)0;
-    int jb = -1, rb = 0;
 #pragma unroll
-    for (int j = 0; j < MAXM; ++j) {
-      const bool avail = (j < M) && !((taken >> j) & 1u);
-      if (avail && (jb < 0 || m[j] < best)) {
-        best = m[j];
-        jb = j;
-        rb = r[j];
+  for (int k = 0; k < MAXM; ++k) {
+    if (k < L && live) {
+      const T d = sqrt_t(km[k]);
+      if (!(d <= tol_pf)) {
+        live = false;  // the reference's break
+      } else {
+        const T q = (tol - d) / tol;
+        Pr = Pr + (Mt + q * q);
+        bool dup = false;  // an earlier (accepted) pair holds the same blob
+#pragma unroll
+        for (int e = 0; e < k; ++e) dup |= kr[e] == kr[k];
+        if (dup) {
+          Pr = Pr - (T)(s * 3);
+          ++s;
+        }
+        if ((fa.downgrade >> kj[k]) & 1u) Pr = Pr - (T)2;
+        if (PAIRS) {
+          pairs[2 * k] = (uint32_t)kj[k] + 1u;
+          pairs[2 * k + 1] = (uint32_t)kr[k] + 1u;
+          *npairs = k + 1;
+        }
       }
-    }
-    const T d = sqrt_t(best);
-    if (!(d <= tol_pf)) break;
-    const T q = (tol - d) / tol;
-    Pr = Pr + (Mt + q * q);
-    bool dup = false;
-#pragma unroll
-    for (int j = 0; j < MAXM; ++j) dup |= ((taken >> j) & 1u) && (r[j] == rb);
-    if (dup) {
-      Pr = Pr - (T)(s * 3);
-      ++s;
-    }
-    if ((fa.downgrade >> jb) & 1u) Pr = Pr - (T)2;
-    taken |= 1u << jb;
-    if (PAIRS) {
-      pairs[2 * k] = (uint32_t)jb + 1u;
-      pairs[2 * k + 1] = (uint32_t)rb + 1u;
-      *npairs = k + 1;
     }
   }
   return Pr;
