@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
-    ap.add_argument("--timing-period", type=int, default=8,
+    ap.add_argument("--timing-period", type=int, default=25,
                     help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream)")
     ap.add_argument("--diag", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
@@ -73,6 +73,19 @@ def pmc_traffic(path: str, kernel: str):
         return row.get("hbm_bytes")
     except (OSError, ValueError):
         return None
+
+
+def combine_ranks(dist, elapsed: float, updates: float):
+    """Whole-job figures: the slowest rank's time (max) and all ranks' particle-updates (sum), over gloo.
+    No data-path collective exists: streams are independent, only these two scalars cross ranks."""
+    if dist is None:
+        return float(elapsed), float(updates)
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    u = torch.tensor([updates], dtype=torch.float64)
+    dist.all_reduce(u, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(u.item())
 
 
 def cpu_baseline(cfg, n_frames: int):
@@ -151,16 +164,7 @@ def main():
     stats = eng.kernel_stats()
     eng.set_option(pf.OPT_TIMING, 0)
 
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        u = torch.tensor([updates], dtype=torch.float64)
-        dist.all_reduce(u, op=dist.ReduceOp.SUM)
-        total_updates = float(u.item())
-    else:
-        total_updates = float(updates)
+    elapsed, total_updates = combine_ranks(dist, elapsed, updates)
 
     if rank == 0:
         S = 48  # fp32 SoA state bytes per particle

@@ -23,11 +23,11 @@
 //  min(B,M) full rescans, O(N^2) cumulative-search stratified resampling): bench.py times it as the
 //  single-thread CPU baseline ("kind": "port").
 //
-//  Parity status: the reference ships NO tests, fixtures or golden vectors and
-//  cannot be compiled here (Eigen/OpenCV/ROS absent).  This restatement is pinned by known-answer
-//  tests derived from the reference source (tests/test_oracle_kat.py: likelihood closed forms,
-//  libstdc++ RNG stream, Philox4x32-10 published vectors) — "parity pinned by KATs only; no reference
-//  run".  Summation order of 4x4 products is sequential k=0..3 (Eigen's packet order is unverifiable
+//  Parity status: PARITY UNPINNED by the reference itself — it ships NO tests, fixtures or golden
+//  vectors and cannot be compiled here (Eigen/OpenCV/ROS absent), so no reference
+//  output exists to check against.  This restatement is instead pinned by known-answer tests derived
+//  from the reference source (tests/test_oracle_kat.py: likelihood closed forms, libstdc++ RNG stream,
+//  Philox4x32-10 published vectors) and frozen as golden fixtures (tests/golden/, make_golden.py).  Summation order of 4x4 products is sequential k=0..3 (Eigen's packet order is unverifiable
 //  here); differences are at the ulp level.
 //
 //  Build: oracle/Makefile  (g++ -O2 -ffp-contract=off, no -march=native: no FMA contraction, so the
