@@ -150,8 +150,11 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *   PFMPE_OPT_RECORD_COUNTS [0|1]  keep counterMeas on device for pfmpe_get_counts
  *   PFMPE_OPT_PRUNE         [1|0]  exact x-window blob pruning in the likelihood (0 = scan all B blobs)
  *   PFMPE_OPT_TIMING        [0|P]  bracket the kernel launches of every P-th frame with HIP events
- *                                  (pfmpe_get_kernel_stats); P = 1 times every frame, 0 is off */
-enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3 };
+ *                                  (pfmpe_get_kernel_stats); P = 1 times every frame, 0 is off
+ *   PFMPE_OPT_FUSED         [1|0]  run a frame as ONE cooperative launch (k_frame) whenever all its
+ *                                  blocks fit on the device at once (default 1); 0 forces the
+ *                                  two-launch path (k_propagate_weigh + k_resample) */
+enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* ----------------------------------------------------------------------- device-resident inputs */
@@ -165,7 +168,8 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* ctx, const double* blobs, const int32_t* of
 enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduce)  */
        PFMPE_K_RESAMPLE = 1,  /* k_resample (+ last-block winner / frame record)     */
        PFMPE_K_AUX = 2,       /* regeneration for pfmpe_get_particles                */
-       PFMPE_K_COUNT = 3 };
+       PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one cooperative launch  */
+       PFMPE_K_COUNT = 4 };
 int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
 int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
 const char* pfmpe_kernel_name(int kernel);

@@ -20,8 +20,8 @@ OK, E_ARG, E_HIP, E_CAP, E_STATE = 0, -1, -2, -3, -4
 STATE_F32, STATE_F64 = 0, 1
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
-OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING = 1, 2, 3
-K_PROPAGATE, K_RESAMPLE, K_AUX, K_COUNT = 0, 1, 2, 3
+OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_COUNT = 0, 1, 2, 3, 4
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (

@@ -39,10 +39,15 @@ namespace pfmpe {
 
 constexpr int kBlock = 256;            // particles per block (4 waves)
 constexpr int kWaves = kBlock / 64;
-constexpr int kGroup = 64;             // blocks per reduction group (one per lane of the group wave)
+// Blocks per reduction group: ~sqrt(blocks), at most kGroup (one per lane of the group wave).  Arrival
+// counters are agent-scope atomics that execute at the memory side and serialise per address (~25 ns
+// each), so sqrt balances the group counters against the top counter (a single 391-way counter cost
+// ~10 us at C2).  A grid of one group skips the top counter: its group wave is the top wave.
+constexpr int kGroup = 64;
 constexpr int kMaxMarkers = 16;
 constexpr int kMaxBlobs = 1024;
 constexpr int kBuckets = 128;          // x-buckets of the blob table
+constexpr int kMaxIter = 4096;         // PF iterations per frame (reference: 80); < 2^16 for k_frame's release tags
 constexpr int kPlanes = 12;            // r00 r01 r02 t0 r10 r11 r12 t1 r20 r21 r22 t2
 
 enum : int { kRngReference = 0, kRngPhilox = 1 };
@@ -64,7 +69,8 @@ struct FrameArgsT {
   uint32_t downgrade;             // bit j: marker j downgraded
   int32_t N, M, B, it;            // particles, markers, blobs, it_since_initialized_
   int32_t cam_identity, max_iter, force_iters, nblk;
-  int32_t ngrp, diag;             // groups; diagnostic switches (0 in production)
+  int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
+  int32_t diag, pad_;             // diagnostic switches (0 in production)
   int64_t ld;                     // SoA plane stride in elements
 };
 
@@ -463,6 +469,14 @@ __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, c
 
 // ----------------------------------------------------------------------------- wave/block helpers
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// Lanes of ONE wave exchanging data through LDS without a workgroup barrier: the hardware keeps a
+// wave's LDS operations in order, but the compiler must also be told that other lanes wrote (else it
+// may forward a lane's own earlier store to its read).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
 // All wave-level scans and reductions run on DPP lane moves (no LDS, no ds_bpermute): row_shr 1/2/4/8
@@ -518,6 +532,9 @@ struct OpMax {
 };
 struct OpMin {
   __device__ double operator()(double a, double b) const { return b < a ? b : a; }
+};
+struct OpMaxI {
+  __device__ int operator()(int a, int b) const { return b > a ? b : a; }
 };
 // inclusive scan x_0 op ... op x_i; `id` is the identity of op
 template <typename V, typename Op>
@@ -722,11 +739,13 @@ __device__ __forceinline__ bool wave_arrive_last(uint32_t* counter, int count) {
 // done, 11 counts done, 12 scatter done, 13-18 finalize phases, 19 earliest table built (min).
 constexpr int kStamps = 32;
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+// per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
+// (min for 0/4/19, max otherwise).  Row 0 holds the single-writer stamps (top / final waves).
 __device__ __forceinline__ void stamp_min(uint64_t* st, int idx, uint64_t t) {
-  if (st) atomicMin((unsigned long long*)(st + idx), (unsigned long long)t);
+  if (st) st[(size_t)(1 + blockIdx.x) * kStamps + idx] = t;
 }
 __device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
-  if (st) atomicMax((unsigned long long*)(st + idx), (unsigned long long)t);
+  if (st) st[(size_t)(1 + blockIdx.x) * kStamps + idx] = t;
 }
 
 // ============================================================================== kernels
@@ -816,68 +835,151 @@ __device__ __forceinline__ void copy_table(const unsigned char* __restrict__ src
   for (int i = threadIdx.x; i < n4; i += kBlock) d4[i] = s4[i];
 }
 
-// ---- group wave of k_propagate_weigh: lanes <-> the <= 64 blocks of group g
-__device__ void propagate_group(int nblk, int g, const BlockPart* __restrict__ part, BlockScan* __restrict__ bscan,
-                                GroupPart* __restrict__ gpart) {
-  const int lane = lane_id();
-  const int b = g * kGroup + lane;
-  const bool vb = b < nblk;
-  double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY, maxw = -INFINITY, minw = INFINITY;
-  int amax = 0x7fffffff, amin = 0x7fffffff;
-  if (vb) {
-    const BlockPart* p = part + b;
-    sum = ld_wt_d(&p->sum);
-    maxrel = ld_wt_d(&p->maxrel);
-    minrel = ld_wt_d(&p->minrel);
-    maxw = ld_wt_d(&p->maxw);
-    minw = ld_wt_d(&p->minw);
-    const uint64_t ai = ld_wt(&p->argmax);
-    amax = lo32(ai);
-    amin = hi32(ai);
-  }
-  const double incl = wave_incl_sum(sum);
-  const double E = wave_shr1(incl, 0.0);  // exclusive prefix = previous lane's inclusive value
-  const double zmax = vb ? E + maxrel : -INFINITY;
-  const double zmin = vb ? E + minrel : INFINITY;
-  const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
-  const double zp_max = wave_shr1(zi_max, -(double)INFINITY), zp_min = wave_shr1(zi_min, (double)INFINITY);
-  if (vb) {
-    BlockScan s;
-    s.E = E;
-    s.zin_max = zp_max;
-    s.zin_min = zp_min;
-    s.pad = 0.0;
-    bscan[b] = s;
-  }
-  const double gsum = lane_value(incl, 63);
-  const double gzmax = lane_value(zi_max, 63), gzmin = lane_value(zi_min, 63);
-  wave_argmax(maxw, amax);
-  wave_argmin(minw, amin);
-  if (lane == 0) {
-    GroupPart* gp = gpart + g;
-    st_wt_d(&gp->sum, gsum);
-    st_wt_d(&gp->zmax, gzmax);
-    st_wt_d(&gp->zmin, gzmin);
-    st_wt_d(&gp->maxw, maxw);
-    st_wt_d(&gp->minw, minw);
-    st_wt(&gp->argmax, pack2(amax, amin));
-  }
+// Control record / scan records move between blocks of one launch (and, in k_frame, between the
+// iterations of one launch) through write-through words only.
+__device__ __forceinline__ Ctrl load_ctrl_wt(const Ctrl* __restrict__ ctrl) {
+  static_assert(sizeof(Ctrl) % 8 == 0, "Ctrl words");
+  Ctrl c;
+  uint64_t* d = (uint64_t*)&c;
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(Ctrl) / 8); ++q) d[q] = ld_wt((const uint64_t*)ctrl + q);
+  return c;
+}
+__device__ __forceinline__ void store_ctrl_wt(Ctrl* __restrict__ ctrl, const Ctrl& c) {
+  const uint64_t* s = (const uint64_t*)&c;
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(Ctrl) / 8); ++q) st_wt((uint64_t*)ctrl + q, s[q]);
+}
+__device__ __forceinline__ Ctrl zero_ctrl() {
+  Ctrl z;
+  z.best_max = 0.0;
+  z.S = 0.0;
+  z.Rmax = 0.0;
+  z.done = z.has_best = z.best_idx = z.best_iter = z.best_slot = z.cur_slot = 0;
+  z.iters = z.kept_slot = z.kept_iter = z.accepted = z.most_likely_idx = z.pad0 = 0;
+  z.K_total = 0;
+  return z;
+}
+__device__ __forceinline__ BlockScan load_bscan_wt(const BlockScan* p) {
+  BlockScan s;
+  s.E = ld_wt_d(&p->E);
+  s.zin_max = ld_wt_d(&p->zin_max);
+  s.zin_min = ld_wt_d(&p->zin_min);
+  s.pad = 0.0;
+  return s;
+}
+__device__ __forceinline__ GroupScan load_gscan_wt(const GroupScan* p) {
+  GroupScan s;
+  s.G = ld_wt_d(&p->G);
+  s.Gin = ld_wt_d(&p->Gin);
+  return s;
 }
 
-// ---- top wave of k_propagate_weigh: iteration bookkeeping, exit rule, group prefixes, accept
+// ---- group wave of the weighing pass: the fa.gsz blocks of group g, 64 per tile (one per lane).
+// Exclusive in-group prefixes E_b are carried across tiles, and so are the exclusive running extrema of
+// z = fl(E_b + in-block prefix) (any fixed association works: k_resample evaluates every c_i and every
+// block-start running max from these same stored E_b).  Returns the group partial.
+__device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, const BlockPart* __restrict__ part,
+                                                     BlockScan* __restrict__ bscan, GroupPart* __restrict__ gpart) {
+  const int lane = lane_id();
+  const int b0 = g * gsz;
+  const int nb = min(gsz, nblk - b0);
+  double cE = 0.0, cmax = -INFINITY, cmin = INFINITY;  // carries
+  double maxw = -INFINITY, minw = INFINITY;
+  int amax = 0x7fffffff, amin = 0x7fffffff;
+  for (int t = 0; t < nb; t += 64) {  // one tile unless gsz > 64
+    const int b = b0 + t + lane;
+    const bool vb = t + lane < nb;
+    double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY;
+    if (vb) {
+      const BlockPart* p = part + b;
+      sum = ld_wt_d(&p->sum);
+      maxrel = ld_wt_d(&p->maxrel);
+      minrel = ld_wt_d(&p->minrel);
+      const uint64_t ai = ld_wt(&p->argmax);
+      cmb_max(maxw, amax, ld_wt_d(&p->maxw), lo32(ai));
+      cmb_min(minw, amin, ld_wt_d(&p->minw), hi32(ai));
+    }
+    const double incl = wave_incl_sum(sum);
+    const double E = cE + wave_shr1(incl, 0.0);  // exclusive prefix within the group
+    const double zmax = vb ? E + maxrel : -INFINITY;
+    const double zmin = vb ? E + minrel : INFINITY;
+    const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
+    double zp_max = wave_shr1(zi_max, -(double)INFINITY), zp_min = wave_shr1(zi_min, (double)INFINITY);
+    zp_max = zp_max > cmax ? zp_max : cmax;
+    zp_min = zp_min < cmin ? zp_min : cmin;
+    if (vb) {
+      BlockScan* s = bscan + b;
+      st_wt_d(&s->E, E);
+      st_wt_d(&s->zin_max, zp_max);
+      st_wt_d(&s->zin_min, zp_min);
+    }
+    cE = cE + lane_value(incl, 63);
+    const double tmax = lane_value(zi_max, 63), tmin = lane_value(zi_min, 63);
+    cmax = tmax > cmax ? tmax : cmax;
+    cmin = tmin < cmin ? tmin : cmin;
+  }
+  wave_argmax(maxw, amax);
+  wave_argmin(minw, amin);
+  GroupPart r;
+  r.sum = cE;
+  r.zmax = cmax;
+  r.zmin = cmin;
+  r.maxw = maxw;
+  r.minw = minw;
+  r.argmax = amax;
+  r.argmin = amin;
+  if (lane == 0) {
+    GroupPart* gp = gpart + g;
+    st_wt_d(&gp->sum, r.sum);
+    st_wt_d(&gp->zmax, r.zmax);
+    st_wt_d(&gp->zmin, r.zmin);
+    st_wt_d(&gp->maxw, r.maxw);
+    st_wt_d(&gp->minw, r.minw);
+    st_wt(&gp->argmax, pack2(amax, amin));
+  }
+  return r;
+}
+
+// group partial g of a weight slot: from memory, or (single-group frames) this iteration's values still
+// in registers
+__device__ __forceinline__ GroupPart group_part(const GroupPart* __restrict__ gp, int g, const GroupPart* regs) {
+  if (regs) return *regs;
+  GroupPart r;
+  r.sum = ld_wt_d(&gp[g].sum);
+  r.zmax = ld_wt_d(&gp[g].zmax);
+  r.zmin = ld_wt_d(&gp[g].zmin);
+  r.maxw = ld_wt_d(&gp[g].maxw);
+  r.minw = ld_wt_d(&gp[g].minw);
+  const uint64_t ai = ld_wt(&gp[g].argmax);
+  r.argmax = lo32(ai);
+  r.argmin = hi32(ai);
+  return r;
+}
+
+// ---- top wave of the weighing pass: iteration bookkeeping, exit rule, group prefixes, accept.  Reads
+// and writes the control record through write-through words.  `gen` (k_frame only) is written last, after
+// everything this wave wrote has drained: the value gen_base + iter + 1 releases the blocks waiting for
+// this iteration's outcome (gen_base = frame sequence << 16, so no stale value can match).
+// cur: this iteration's group partial when the frame has a single group (the group wave is the top).
 template <typename T, int RNG>
-__device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __restrict__ ctrl, int iter,
-                              const GroupPart* __restrict__ gp0, const GroupPart* __restrict__ gp1,
-                              GroupScan* __restrict__ gscan) {
+__device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __restrict__ ctrl, int iter,
+                                              const GroupPart* __restrict__ gp0, const GroupPart* __restrict__ gp1,
+                                              GroupScan* __restrict__ gscan, uint32_t* __restrict__ gen,
+                                              uint32_t gen_base, const GroupPart* cur) {
   const int lane = lane_id();
   const int ngrp = fa.ngrp;
+  const Ctrl c0 = load_ctrl_wt(ctrl);
   const int slot = c0.cur_slot;
   // this iteration's max / first argmax
   double mv = -INFINITY;
   int mi = 0x7fffffff;
   {
     const GroupPart* P = slot ? gp1 : gp0;
-    for (int g = lane; g < ngrp; g += 64) cmb_max(mv, mi, ld_wt_d(&P[g].maxw), lo32(ld_wt(&P[g].argmax)));
+    for (int g = lane; g < ngrp; g += 64) {
+      const GroupPart q = group_part(P, g, cur);
+      cmb_max(mv, mi, q.maxw, q.argmax);
+    }
     wave_argmax(mv, mi);
   }
   Ctrl c = c0;
@@ -892,119 +994,115 @@ __device__ void propagate_top(const FrameArgsT<T>& fa, const Ctrl& c0, Ctrl* __r
   const bool go_on = fa.force_iters > 0 ? (c.iters < fa.force_iters)
                                         : (c.iters < fa.max_iter && mv < fa.exit_thr);  // PE:616
   c.cur_slot = c.has_best ? 1 - c.best_slot : 1 - slot;
-  if (go_on) {
-    if (lane == 0) *ctrl = c;
-    return;
-  }
-  c.done = 1;
-  c.kept_slot = c.has_best ? c.best_slot : slot;
-  c.kept_iter = c.has_best ? c.best_iter : iter;
-  const GroupPart* KG = c.kept_slot ? gp1 : gp0;
+  if (!go_on) {
+    c.done = 1;
+    c.kept_slot = c.has_best ? c.best_slot : slot;
+    c.kept_iter = c.has_best ? c.best_iter : iter;
+    const GroupPart* KG = c.kept_slot ? gp1 : gp0;
+    const GroupPart* kreg = (c.kept_slot == slot) ? cur : nullptr;
 
-  // group prefixes G_g (tiles of 64 groups, carried), S = total
-  double carry = 0.0;
-  for (int base = 0; base < ngrp; base += 64) {
-    const int g = base + lane;
-    const double s = g < ngrp ? ld_wt_d(&KG[g].sum) : 0.0;
-    const double incl = wave_incl_sum(s);
-    const double prev = wave_shr1(incl, 0.0);
-    const double G = lane == 0 ? carry : carry + prev;
-    if (g < ngrp) gscan[g].G = G;
-    carry = carry + lane_value(incl, 63);
-  }
-  const double S = carry;
-  // running max of c at each group start: Gin_g = max over earlier groups of fl(fl(G + z)/S)
-  double run = -INFINITY;
-  if (S != 0.0) {
+    // S = total over groups (tiles of 64 groups, carried)
+    double carry = 0.0;
     for (int base = 0; base < ngrp; base += 64) {
       const int g = base + lane;
+      const double s = g < ngrp ? group_part(KG, g, kreg).sum : 0.0;
+      carry = carry + lane_value(wave_incl_sum(s), 63);
+    }
+    const double S = carry;
+    // group prefixes G_g (same association as above, recomputed) and the running max of c at each group
+    // start: Gin_g = max over earlier groups of fl(fl(G + z)/S)
+    double run = -INFINITY;
+    carry = 0.0;
+    for (int base = 0; base < ngrp; base += 64) {
+      const int g = base + lane;
+      GroupPart q;
+      q.sum = 0.0;
+      q.zmax = -INFINITY;
+      q.zmin = INFINITY;
+      if (g < ngrp) q = group_part(KG, g, kreg);
+      const double incl = wave_incl_sum(q.sum);
+      const double prev = wave_shr1(incl, 0.0);
+      const double G = lane == 0 ? carry : carry + prev;
+      carry = carry + lane_value(incl, 63);
       double cm = -INFINITY;
-      if (g < ngrp) {
-        const double z = S > 0.0 ? ld_wt_d(&KG[g].zmax) : ld_wt_d(&KG[g].zmin);
-        cm = (gscan[g].G + z) / S;
-      }
+      if (g < ngrp && S != 0.0) cm = (G + (S > 0.0 ? q.zmax : q.zmin)) / S;
       const double im = wave_incl_max(cm);
       double ex = wave_shr1(im, -(double)INFINITY);
       ex = ex > run ? ex : run;
-      if (g < ngrp) gscan[g].Gin = ex;
+      if (g < ngrp) {
+        st_wt_d(&gscan[g].G, G);
+        st_wt_d(&gscan[g].Gin, ex);
+      }
       const double tm = lane_value(im, 63);
       run = tm > run ? tm : run;
     }
-  }
-  // kept iteration's argmax / argmin (re-init branch, PE:714)
-  double amv = -INFINITY, anv = INFINITY;
-  int ami = 0x7fffffff, ani = 0x7fffffff;
-  for (int g = lane; g < ngrp; g += 64) {
-    const uint64_t ai = ld_wt(&KG[g].argmax);
-    cmb_max(amv, ami, ld_wt_d(&KG[g].maxw), lo32(ai));
-    cmb_min(anv, ani, ld_wt_d(&KG[g].minw), hi32(ai));
-  }
-  wave_argmax(amv, ami);
-  wave_argmin(anv, ani);
-  if (lane == 0) {
+    if (S == 0.0) run = -INFINITY;
+    // kept iteration's argmax / argmin (re-init branch, PE:714)
+    double amv = -INFINITY, anv = INFINITY;
+    int ami = 0x7fffffff, ani = 0x7fffffff;
+    for (int g = lane; g < ngrp; g += 64) {
+      const GroupPart q = group_part(KG, g, kreg);
+      cmb_max(amv, ami, q.maxw, q.argmax);
+      cmb_min(anv, ani, q.minw, q.argmin);
+    }
+    wave_argmax(amv, ami);
+    wave_argmin(anv, ani);
     const double highest = c.has_best ? c.best_max : 0.0;
     c.S = S;
     c.Rmax = run;
     c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
     if (c.accepted) {
       c.most_likely_idx = c.best_idx;
-      c.K_total = count_targets<T, RNG>(fa, c.iters, run);
+      c.K_total = lane == 0 ? count_targets<T, RNG>(fa, c.iters, run) : 0;
     } else {
       // argmax of the normalised weights (PE:714): a negative sum flips the order
       c.most_likely_idx = (S < 0.0) ? ani : ami;
       c.K_total = 0;
     }
-    *ctrl = c;
+  }
+  if (lane == 0) {
+    store_ctrl_wt(ctrl, c);
+    if (gen) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ctrl / gscan words drained before the release
+      __hip_atomic_store((gu32_t*)gen, gen_base + (uint32_t)iter + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
-// ---- launch 1: motion + projection + likelihood, one particle per thread
+// ---- one particle through the motion model, projection and likelihood (PE:543-604, PE:2385)
 template <typename T, int RNG, int MAXM, bool PRUNE>
-__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
-    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ w0,
-    T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
-    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
-    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
-    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, int iter, uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ LdsConst<T> sc;
-  __shared__ double s_tot[kWaves], s_rmax[kWaves], s_rmin[kWaves], s_mx[kWaves], s_mn[kWaves];
-  __shared__ int s_ix[kWaves], s_in[kWaves];
-
-  if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
-  const int n = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = n < fa.N;
-  // table loads first: vmcnt retires in order, so the LDS copy then waits only for them while the
-  // prior loads stay in flight across the barrier
-  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
-  T A[12];
-  if (valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c0 = *ctrl;
-  if (c0.done) return;  // the exit rule already fired (uniform)
-  const int slot = c0.cur_slot;
-  stage_consts(fa, sc);
-  __syncthreads();  // table + constants visible
-  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
-  if (stamps && threadIdx.x == 0) {
-    const uint64_t t = rt_now();
-    stamp_max(stamps, 8, t);
-    stamp_min(stamps, 19, t);
-  }
-
+__device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
+                                            const T* A, int n, int iter, T* P) {
+  T u[MAXM], v[MAXM];
+  propagate<T, RNG>(fa, sc, A, n, iter, P);
+  project_markers<T, MAXM>(fa, sc, P, u, v);
   T w = (T)0;
-  if (valid) {
-    T P[12], u[MAXM], v[MAXM];
-    propagate<T, RNG>(fa, sc, A, n, iter, P);
-    project_markers<T, MAXM>(fa, sc, P, u, v);
-    if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
-      T m[MAXM];
-      int r[MAXM];
-      column_minima<T, MAXM, PRUNE>(fa, u, v, tb.bx, tb.by, tb.orig, tb.bstart, tb.xmin, tb.inv_bw, m, r);
-      w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
-    }
-    (slot ? w1 : w0)[n] = w;
+  if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
+    T m[MAXM];
+    int r[MAXM];
+    column_minima<T, MAXM, PRUNE>(fa, u, v, tb.bx, tb.by, tb.orig, tb.bstart, tb.xmin, tb.inv_bw, m, r);
+    w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
   }
-  if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
+  return w;
+}
+
+// LDS scratch of the per-iteration partials
+struct WeighLds {
+  double tot[kWaves], rmax[kWaves], rmin[kWaves], mx[kWaves], mn[kWaves];
+  int ix[kWaves], in_[kWaves];
+};
+
+// ---- the iteration's partials: wave -> block (write-through + counter) -> group -> top.  Called by
+// every thread (one barrier inside).  On return only wave 0 may have done hand-off work.
+template <typename T, int RNG>
+__device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, bool valid, int n, int slot, int iter,
+                                                  WeighLds& sh, BlockPart* __restrict__ part0,
+                                                  BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0,
+                                                  BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+                                                  GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                                  Ctrl* __restrict__ ctrl, uint32_t* __restrict__ gcount,
+                                                  uint32_t* __restrict__ tcount, uint32_t* __restrict__ gen,
+                                                  uint32_t gen_base, uint64_t* __restrict__ stamps) {
   // wave partials: scan total, extrema of the wave-inclusive prefix, max/argmax, min/argmin
   const double wd = valid ? (double)w : 0.0;
   const double wi = wave_incl_sum(wd);
@@ -1015,35 +1113,35 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   wave_argmax(mx, ix);
   wave_argmin(mn, in_);
   const int lane = lane_id(), wv = wave_id();
-  if (lane == 63) s_tot[wv] = wi;
+  if (lane == 63) sh.tot[wv] = wi;
   if (lane == 0) {
-    s_rmax[wv] = rmx;
-    s_rmin[wv] = rmn;
-    s_mx[wv] = (double)mx;
-    s_mn[wv] = (double)mn;
-    s_ix[wv] = ix;
-    s_in[wv] = in_;
+    sh.rmax[wv] = rmx;
+    sh.rmin[wv] = rmn;
+    sh.mx[wv] = (double)mx;
+    sh.mn[wv] = (double)mn;
+    sh.ix[wv] = ix;
+    sh.in_[wv] = in_;
   }
   __syncthreads();
-  if (wv != 0) return;  // waves 1..3 are done; wave 0 publishes and (maybe) reduces
+  if (wv != 0) return;
 
-  const int g = blockIdx.x / kGroup;
-  const int gsize = min(kGroup, fa.nblk - g * kGroup);
+  const int g = blockIdx.x / fa.gsz;
+  const int gsize = min(fa.gsz, fa.nblk - g * fa.gsz);
   int last = 0;
   if (lane == 0) {
     // block partial, same association as block_incl_sum: pre_w = ((0 + t0) + t1) + ...
-    double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = s_mx[0], bmn = s_mn[0];
-    int bix = s_ix[0], bin = s_in[0];
+    double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = sh.mx[0], bmn = sh.mn[0];
+    int bix = sh.ix[0], bin = sh.in_[0];
 #pragma unroll
     for (int ww = 0; ww < kWaves; ++ww) {
-      const double a = pre + s_rmax[ww], b = pre + s_rmin[ww];
+      const double a = pre + sh.rmax[ww], b = pre + sh.rmin[ww];
       maxrel = a > maxrel ? a : maxrel;
       minrel = b < minrel ? b : minrel;
       if (ww) {
-        cmb_max(bmx, bix, s_mx[ww], s_ix[ww]);
-        cmb_min(bmn, bin, s_mn[ww], s_in[ww]);
+        cmb_max(bmx, bix, sh.mx[ww], sh.ix[ww]);
+        cmb_min(bmn, bin, sh.mn[ww], sh.in_[ww]);
       }
-      pre = pre + s_tot[ww];
+      pre = pre + sh.tot[ww];
     }
     BlockPart* bp = (slot ? part1 : part0) + blockIdx.x;
     st_wt_d(&bp->sum, pre);
@@ -1056,18 +1154,62 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     last = arrive_last(gcount + g, gsize) ? 1 : 0;
   }
   if (!lane_value(last, 0)) return;
-  propagate_group(fa.nblk, g, slot ? part1 : part0, slot ? bscan1 : bscan0, slot ? gpart1 : gpart0);
-  if (!wave_arrive_last(tcount, fa.ngrp)) return;
+  const GroupPart gr =
+      propagate_group(fa.nblk, fa.gsz, g, slot ? part1 : part0, slot ? bscan1 : bscan0, slot ? gpart1 : gpart0);
+  const bool single = fa.ngrp == 1;
+  if (!single && !wave_arrive_last(tcount, fa.ngrp)) return;
   if (stamps && lane == 0) stamps[2] = rt_now();
-  propagate_top<T, RNG>(fa, c0, ctrl, iter, gpart0, gpart1, gscan);
+  propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, gen, gen_base, single ? &gr : nullptr);
   if (stamps && lane == 0) stamps[3] = rt_now();
+}
+
+// ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread
+template <typename T, int RNG, int MAXM, bool PRUNE>
+__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ w0,
+    T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, int iter, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds sh;
+
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  // table loads first: vmcnt retires in order, so the LDS copy then waits only for them while the
+  // prior loads stay in flight across the barrier
+  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  const Ctrl c0 = *ctrl;  // written by the previous launch
+  if (c0.done) return;    // the exit rule already fired (uniform)
+  const int slot = c0.cur_slot;
+  stage_consts(fa, sc);
+  __syncthreads();  // table + constants visible
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  if (stamps && threadIdx.x == 0) {
+    const uint64_t t = rt_now();
+    stamp_max(stamps, 8, t);
+    stamp_min(stamps, 19, t);
+  }
+  T w = (T)0;
+  if (valid) {
+    T P[12];
+    w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
+    (slot ? w1 : w0)[n] = w;
+  }
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
+  publish_iteration<T, RNG>(fa, w, valid, n, slot, iter, sh, part0, part1, bscan0, bscan1, gpart0, gpart1, gscan,
+                            ctrl, gcount, tcount, nullptr, 0u, stamps);
 }
 
 // ---- winner + frame record (one wave).  Writes into pinned host memory, then resets the control
 // record for the next frame.  Lanes 0-31 regenerate the most likely particle and lanes 32-63 the winner
 // in one pass; the winner's column minima run over blobs held one per lane (loaded once).
 template <typename T, int RNG, int MAXM>
-__device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
+__device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
                                const unsigned char* __restrict__ table, const T* __restrict__ prior, int winner,
                                OutDev& rec, OutDev* __restrict__ out, int32_t tag, uint64_t* __restrict__ stamps) {
   const int lane = lane_id();
@@ -1092,6 +1234,7 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
   }
   if (stamps && lane == 0) stamps[13] = stamps[14] = rt_now();
   if (lane < 2 * kMaxMarkers) rec.corr[lane] = 0u;
+  wave_lds_sync();  // lane 0 writes the pairs over the cleared words below
   int np = 0;
   if (c.accepted) {
     T u[MAXM], v[MAXM], m[MAXM];
@@ -1162,8 +1305,7 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
     rec.n_corr = np;
     if (stamps) stamps[17] = rt_now();
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  wave_lds_sync();
   constexpr int kWords = (int)(offsetof(OutDev, kept_slot) / 8);
   static_assert(offsetof(OutDev, kept_slot) % 8 == 0 && kWords <= 64, "record layout");
   if (lane < kWords) st_sys64((uint64_t*)out + lane, ((const uint64_t*)&rec)[lane]);
@@ -1172,90 +1314,65 @@ __device__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, c
   publish_tag(&out->tag, tag);
   if (stamps) stamps[18] = rt_now();
   // the next frame starts from the all-zero control record
-  Ctrl z;
-  z.best_max = 0.0;
-  z.S = 0.0;
-  z.Rmax = 0.0;
-  z.done = z.has_best = z.best_idx = z.best_iter = z.best_slot = z.cur_slot = 0;
-  z.iters = z.kept_slot = z.kept_iter = z.accepted = z.most_likely_idx = z.pad0 = 0;
-  z.K_total = 0;
-  *ctrl = z;
+  store_ctrl_wt(ctrl, zero_ctrl());
 }
 
-// ---- launch 2: stratified resampling: scan + target counts + wave-cooperative scatter of regenerated
-// particles; the last group's wave picks the winner and writes the frame record
-template <typename T, int RNG, int MAXM>
-__global__ __launch_bounds__(kBlock) void k_resample(
-    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const T* __restrict__ prior,
-    T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
-    const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
-    CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
-    uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
-  __shared__ LdsConst<T> sc;
-  __shared__ OutDev rec;
-  __shared__ double s_sum[kWaves];
-  __shared__ double s_max[kWaves];
-  __shared__ int s_hi[kWaves];
-  __shared__ int s_c[kWaves], s_ci[kWaves];
+// LDS scratch of the resampling phase: scan partials, and per wave the staging of the scatter (the
+// wave's 64 kept particles as rows, and the slot -> owner-lane map of the current 64-slot chunk)
+template <typename T>
+struct ResampleLds {
+  double sum[kWaves], max[kWaves];
+  int hi[kWaves], c[kWaves], ci[kWaves];
+  struct alignas(16) Row {
+    T q[12];
+  } rows[kWaves][64];
+  int map[kWaves][64];
+};
 
-  if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
+// ---- stratified resampling of one block (PE:666-682) + count partials -> winner -> frame record.
+// wd: the thread's kept raw weight (0 for invalid lanes); P: its kept propagated particle when have_P,
+// else regenerated here from A (P_in unused).  Called by every thread; the caller checked c.done && c.accepted.
+template <typename T, int RNG, int MAXM>
+__device__ __forceinline__ void resample_phase(
+    const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
+    const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ post, double wd, const T* A,
+    const T* P_in, bool have_P, const BlockScan& bs, const GroupScan& gs, ResampleLds<T>& sh, OutDev& rec,
+    CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
+    uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq,
+    uint64_t* __restrict__ stamps) {
   const int N = fa.N;
   const int blk = blockIdx.x, lane = lane_id(), wv = wave_id();
-  const int g = blk / kGroup;
+  const int g = blk / fa.gsz;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < N;
-  // Everything that does not depend on the control record is requested first (both weight slots: the
-  // kept one is known only from ctrl), so the loads overlap the ctrl read.
-  T wt0 = (T)0, wt1 = (T)0;
-  if (valid) {
-    wt0 = w0[n];
-    wt1 = w1[n];
-  }
-  const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
-  const GroupScan gs = gscan[g];
-  T A[12];
-  if (valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c = *ctrl;
-  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
-    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
-    return;
-  }
-  stage_consts(fa, sc);  // visible after block_incl_sum's barrier (finalize below: same wave)
-  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
-    if (blockIdx.x == 0 && threadIdx.x < 64)
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
-    return;
-  }
-  const int slot = c.kept_slot, kiter = c.kept_iter, iters = c.iters;
+  const int kiter = c.kept_iter, iters = c.iters;
   const double S = c.S;
   const int64_t Kt = c.K_total;
-  const BlockScan bs = slot ? bsb : bsa;
 
-  const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   double incl;
-  block_incl_sum(wd, incl, s_sum);
+  block_incl_sum(wd, incl, sh.sum);
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 10, rt_now());
   const double cn = (gs.G + (bs.E + incl)) / S;
   // running max of c seeded by the exact running max at the block start:
   // max(Gin_g, fl(fl(G_g + zin_b)/S)); zin_b = -inf (S > 0) / +inf (S < 0) for a group's first block
   const double zin = S > 0.0 ? bs.zin_max : bs.zin_min;
-  const bool first_in_group = (blk % kGroup) == 0;
+  const bool first_in_group = (blk % fa.gsz) == 0;
   double rin = gs.Gin;
   if (!first_in_group) {
     const double cz = (gs.G + zin) / S;
     rin = cz > rin ? cz : rin;
   }
   const double rm = wave_incl_max(valid ? cn : -INFINITY);
-  if (lane == 63) s_max[wv] = rm;
+  if (lane == 63) sh.max[wv] = rm;
   __syncthreads();
   double pm = rin;
-  for (int w = 0; w < wv; ++w) pm = s_max[w] > pm ? s_max[w] : pm;
+  for (int w = 0; w < wv; ++w) pm = sh.max[w] > pm ? sh.max[w] : pm;
   const double R = rm > pm ? rm : pm;
   const int hi = valid ? (int)count_targets<T, RNG>(fa, iters, R) : N;
-  if (lane == 63) s_hi[wv] = hi;
+  if (lane == 63) sh.hi[wv] = hi;
   __syncthreads();
   int lo = wave_shr1(hi, 0);
-  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : s_hi[wv - 1];
+  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : sh.hi[wv - 1];
   const int cntn = valid ? hi - lo : 0;
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 11, rt_now());
   if (counts && valid) counts[n] = (uint32_t)cntn;
@@ -1283,34 +1400,48 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     int ci = valid ? n : 0x7fffffff;
     wave_argmax(cv, ci);
     if (lane == 0) {
-      s_c[wv] = cv;
-      s_ci[wv] = ci;
+      sh.c[wv] = cv;
+      sh.ci[wv] = ci;
     }
   }
 
-  // regenerate the kept-iteration particle (only lanes that own slots touch the prior)
+  if (stamps && threadIdx.x == 0) stamp_max(stamps, 20, rt_now());
+  // the kept-iteration particle (regenerated only by lanes that own slots)
   T P[12];
 #pragma unroll
-  for (int q = 0; q < 12; ++q) P[q] = (T)0;
-  if (e > a) propagate<T, RNG>(fa, sc, A, n, kiter, P);
+  for (int q = 0; q < 12; ++q) P[q] = have_P ? P_in[q] : (T)0;
+  if (!have_P && e > a) propagate<T, RNG>(fa, sc, A, n, kiter, P);
 
-  // wave-cooperative scatter: the wave's lanes own consecutive slot ranges [a, e)
+  // Wave-cooperative scatter.  The wave's lanes own consecutive slot ranges [a, e) (empty lanes have
+  // a = e = the next start), so slot k belongs to the highest non-empty lane whose start is <= k.  Per
+  // 64-slot chunk: starts inside the chunk mark their lane in an LDS map, a DPP max-scan (carried
+  // across chunks) fills every slot's owner, and the slot lane reads the owner's row from LDS.
   const int wa = lane_value(a, 0);
   const int we = lane_value(e, 63);
-  for (int base = wa; base < we; base += 64) {
-    const int k = base + lane;
-    int l = 0;
+  if (we > wa) {
+    auto& rows = sh.rows[wv];
+    int* map = sh.map[wv];
 #pragma unroll
-    for (int step = 32; step > 0; step >>= 1) {
-      const int ac = __shfl(a, l + step, 64);
-      if (ac <= k) l += step;
-    }
-    T Q[12];
+    for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];
+    int carry = -1;
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 21, rt_now());
+    for (int base = wa; base < we; base += 64) {
+      map[lane] = -1;
+      wave_lds_sync();
+      const int d = a - base;
+      if (e > a && d >= 0 && d < 64) map[d] = lane;
+      wave_lds_sync();
+      int own = map[lane];
+      own = wave_scan(own, -1, OpMaxI());
+      own = own > carry ? own : carry;
+      carry = lane_value(own, 63);
+      const int k = base + lane;
+      wave_lds_sync();  // rows (before the loop) and this chunk's map reads are done before the next clear
+      if (k < we) {
+        const auto& row = rows[own];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) Q[q] = __shfl(P[q], l, 64);
-    if (k < we) {
-#pragma unroll
-      for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = Q[q];
+        for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = row.q[q];
+      }
     }
   }
 
@@ -1319,35 +1450,210 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   if (wv != 0) return;
   int last = 0;
   if (lane == 0) {
-    int bv = s_c[0], bi = s_ci[0];
-    for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, s_c[w], s_ci[w]);
+    int bv = sh.c[0], bi = sh.ci[0];
+    for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
     st_wt(cpart + blk, pack2(bv, bi));
     if (stamps) stamp_max(stamps, 5, rt_now());
-    last = arrive_last(gcount + g, min(kGroup, fa.nblk - g * kGroup)) ? 1 : 0;
+    last = arrive_last(gcount + g, min(fa.gsz, fa.nblk - g * fa.gsz)) ? 1 : 0;
   }
   if (!lane_value(last, 0)) return;
-  {  // group: max count over its blocks
-    const int b = g * kGroup + lane;
-    int bv = -1, bi = 0x7fffffff;
-    if (b < fa.nblk) {
-      const uint64_t cp = ld_wt(cpart + b);
-      bv = lo32(cp);
-      bi = hi32(cp);
+  // group: max count over its blocks (first index on ties)
+  int bv = -1, bi = 0x7fffffff;
+  {
+    const int b0 = g * fa.gsz, nb = min(fa.gsz, fa.nblk - b0);
+    for (int t = lane; t < nb; t += 64) {
+      const uint64_t cp = ld_wt(cpart + b0 + t);
+      cmb_max(bv, bi, lo32(cp), hi32(cp));
     }
     wave_argmax(bv, bi);
-    if (lane == 0) st_wt(cgroup + g, pack2(bv, bi));
   }
-  if (!wave_arrive_last(tcount, fa.ngrp)) return;
+  if (fa.ngrp > 1) {
+    if (lane == 0) st_wt(cgroup + g, pack2(bv, bi));
+    if (!wave_arrive_last(tcount, fa.ngrp)) return;
+    bv = -1;
+    bi = 0x7fffffff;
+    for (int gg = lane; gg < fa.ngrp; gg += 64) {
+      const uint64_t cp = ld_wt(cgroup + gg);
+      cmb_max(bv, bi, lo32(cp), hi32(cp));
+    }
+    wave_argmax(bv, bi);
+  }
   if (stamps && lane == 0) stamps[6] = rt_now();
   // winner = argmax resample count, first index (PE:685-686)
-  int bv = -1, bi = 0x7fffffff;
-  for (int gg = lane; gg < fa.ngrp; gg += 64) {
-    const uint64_t cp = ld_wt(cgroup + gg);
-    cmb_max(bv, bi, lo32(cp), hi32(cp));
-  }
-  wave_argmax(bv, bi);
   finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, bi, rec, out, 2 * seq + 1, stamps);
   if (stamps && lane == 0) stamps[7] = rt_now();
+}
+
+// ---- launch 2 of the two-launch path: stratified resampling + winner + frame record
+template <typename T, int RNG, int MAXM>
+__global__ __launch_bounds__(kBlock) void k_resample(
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const T* __restrict__ prior,
+    T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+    const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
+    CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
+    uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  __shared__ LdsConst<T> sc;
+  __shared__ OutDev rec;
+  __shared__ ResampleLds<T> sh;
+
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
+  const int blk = blockIdx.x;
+  const int g = blk / fa.gsz;
+  const int n = blk * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  // Everything that does not depend on the control record is requested first (both weight slots: the
+  // kept one is known only from ctrl), so the loads overlap the ctrl read.
+  T wt0 = (T)0, wt1 = (T)0;
+  if (valid) {
+    wt0 = w0[n];
+    wt1 = w1[n];
+  }
+  const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
+  const GroupScan gs = gscan[g];
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  const Ctrl c = *ctrl;
+  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
+    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
+    return;
+  }
+  stage_consts(fa, sc);  // visible after block_incl_sum's barrier (finalize below: same wave)
+  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+      wave_lds_sync();
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
+    }
+    return;
+  }
+  const int slot = c.kept_slot;
+  const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
+  const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
+  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec,
+                               cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+}
+
+// ---- the whole frame in ONE cooperative launch (every block co-resident, checked by the host): the
+// PF iterations, the normalisation hand-off and the resampling.  Between the weighing pass and its
+// outcome every block waits for the top wave's release of `gen`; the particle's prior, propagated pose
+// and weight stay in registers across the wait, so nothing is re-read or regenerated (unless the kept
+// iteration is an earlier one).  A wait longer than ~2 s abandons the frame (no record: host error).
+struct FrameLds {
+  Ctrl c;
+  BlockScan bs[2];  // this block's scan words, both weight slots
+  GroupScan gs;
+  int abort;
+};
+
+template <typename T, int RNG, int MAXM, bool PRUNE>
+__global__ __launch_bounds__(kBlock) void k_frame(
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior,
+    T* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
+    BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1,
+    GroupPart* __restrict__ gpart0, GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+    Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup,
+    uint32_t* __restrict__ gcount_w, uint32_t* __restrict__ tcount_w, uint32_t* __restrict__ gcount_r,
+    uint32_t* __restrict__ tcount_r, uint32_t* __restrict__ gen, uint32_t* __restrict__ counts,
+    OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds wsh;
+  __shared__ ResampleLds<T> rsh;
+  __shared__ OutDev rec;
+  __shared__ FrameLds fsh;
+
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  const int lane = lane_id(), wv = wave_id();
+  const int blk = blockIdx.x, g = blk / fa.gsz;
+
+  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  const uint32_t gen_base = ((uint32_t)seq & 0xffffu) << 16;  // iteration release values of this frame
+  Ctrl c = load_ctrl_wt(ctrl);  // the all-zero start-of-frame record (previous launch)
+  stage_consts(fa, sc);
+  __syncthreads();
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  if (stamps && threadIdx.x == 0) {
+    const uint64_t t = rt_now();
+    stamp_max(stamps, 8, t);
+    stamp_min(stamps, 19, t);
+  }
+
+  T P[12], w = (T)0;
+  int iter = 0;
+  for (;; ++iter) {
+    const int slot = c.cur_slot;
+    if (valid) {
+      w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
+      (slot ? w1 : w0)[n] = w;
+    }
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
+    publish_iteration<T, RNG>(fa, w, valid, n, slot, iter, wsh, part0, part1, bscan0, bscan1, gpart0, gpart1, gscan,
+                              ctrl, gcount_w, tcount_w, gen, gen_base, stamps);
+    // wait for this iteration's outcome
+    if (wv == 0) {
+      int ab = 0;
+      if (lane == 0) {
+        const uint32_t want = gen_base + (uint32_t)iter + 1u;
+        const uint64_t t0 = rt_now();
+        while (__hip_atomic_load((gu32_t*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+          __builtin_amdgcn_s_sleep(2);
+          if (rt_now() - t0 > 200000000ull) {  // 2 s at 100 MHz
+            ab = 1;
+            break;
+          }
+        }
+      }
+      ab = lane_value(ab, 0);
+      if (!ab) {
+        // one round trip: the control record's words, this block's scan words (both slots) and its
+        // group's (the scan words are meaningful once the frame is done)
+        constexpr int kCw = (int)(sizeof(Ctrl) / 8);
+        static_assert(sizeof(Ctrl) % 8 == 0 && kCw + 8 <= 64, "Ctrl words");
+        const uint64_t* src = nullptr;
+        uint64_t* dst = nullptr;
+        if (lane < kCw) {
+          src = (const uint64_t*)ctrl + lane;
+          dst = (uint64_t*)&fsh.c + lane;
+        } else if (lane < kCw + 6) {
+          const int sl = (lane - kCw) / 3, q = (lane - kCw) % 3;
+          src = (const uint64_t*)((sl ? bscan1 : bscan0) + blk) + q;
+          dst = (uint64_t*)&fsh.bs[sl] + q;
+        } else if (lane < kCw + 8) {
+          src = (const uint64_t*)(gscan + g) + (lane - kCw - 6);
+          dst = (uint64_t*)&fsh.gs + (lane - kCw - 6);
+        }
+        if (src) *dst = ld_wt(src);
+      }
+      if (lane == 0) fsh.abort = ab;
+    }
+    __syncthreads();
+    if (fsh.abort) return;
+    c = fsh.c;
+    if (c.done) break;
+  }
+
+  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
+    if (blk == 0 && wv == 0)
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
+    return;
+  }
+  const int kslot = c.kept_slot;
+  const bool have_P = c.kept_iter == iter;
+  double wd = 0.0;
+  if (valid) {
+    if (have_P) {
+      wd = (double)w;
+    } else {  // the kept iteration is an earlier one: its weight is in the other slot (own write)
+      wd = (double)(kslot ? w1 : w0)[n];  // this thread's own earlier store
+    }
+  }
+  const BlockScan bs = fsh.bs[kslot];
+  const GroupScan gs = fsh.gs;
+  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, cpart,
+                               cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path)

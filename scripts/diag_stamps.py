@@ -5,11 +5,13 @@ import pf_monocular_pose_estimator_amd as pf
 from pf_monocular_pose_estimator_amd import synthetic as syn
 lib = pf.load()
 lib.pfmpe_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+fused = int(os.environ.get('PFMPE_FUSED', '1'))
 for N in [int(x) for x in sys.argv[1:]] or [100000]:
     cfg = syn.StreamConfig("C2", M=5, B=50, N=N)
     st = syn.make_stream(cfg, 30)
     eng = pf.Engine(0, N); eng.set_model(st.markers, st.K); eng.set_params(pf.default_params()); eng.set_prior(st.prior())
     eng.set_option(99, 4)
+    eng.set_option(pf.OPT_FUSED, fused)
     rows = []
     for fr in st.frames:
         lib.pfmpe_debug_stamps(eng.ctx, None)
@@ -19,10 +21,13 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
         t0 = t[0]
         rows.append([(t[i] - t0) / 100.0 if t[i] else float('nan') for i in range(32)])  # us (100 MHz)
     r = np.median(np.array(rows[5:]), axis=0)
+    if not (r[4] < 1e6):
+        r[4] = float('nan')  # fused frame: no second launch
     print(f"N={N}: K1 start 0 | last arrival {r[1]:.2f} | reduce {r[2]:.2f}->{r[3]:.2f} ({r[3]-r[2]:.2f}) || K2 start {r[4]:.2f} | last arrival {r[5]:.2f} | final {r[6]:.2f}->{r[7]:.2f} ({r[7]-r[6]:.2f})  [us]")
     names = {8: "K1 table built (last)", 19: "K1 table built (first)", 9: "K1 weights (last)", 10: "K2 scan (last)",
              11: "K2 counts (last)", 12: "K2 scatter (last)", 13: "fin Pm", 14: "fin P", 15: "fin minima",
-             16: "fin score", 17: "fin record", 18: "fin published"}
+             16: "fin score", 17: "fin record", 18: "fin published", 20: "K2 block argmax (last)",
+             21: "K2 rows staged (last)", 1: "K1 block partial (last)", 5: "K2 block partial (last)"}
     for i in sorted(names, key=lambda i: r[i]):
         print(f"    {names[i]:24s} {r[i]:8.2f}")
     eng.close()

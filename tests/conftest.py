@@ -20,5 +20,5 @@ def _built_libraries():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     lib = os.path.join(ROOT, "pf_monocular_pose_estimator_amd", "libpfmpe.so")
     if not os.path.exists(lib) and os.path.exists("/opt/rocm/bin/hipcc"):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "pf_monocular_pose_estimator_amd")], check=True)
+        subprocess.run(["make", "-s", "-j5", "-C", os.path.join(ROOT, "pf_monocular_pose_estimator_amd")], check=True)
     yield

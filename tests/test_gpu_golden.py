@@ -19,7 +19,8 @@ INT_KEYS = ("iters", "kept_iter", "accepted", "resampled", "most_likely_idx", "w
 
 @pytest.mark.parametrize("name", STREAMS)
 @pytest.mark.parametrize("bank", [False, True])
-def test_engine_reproduces_fixture(name, bank):
+@pytest.mark.parametrize("fused", [True, False])
+def test_engine_reproduces_fixture(name, bank, fused):
     g = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
     N = g["prior0"].shape[0]
     eng = pf.Engine(device=0, max_particles=N, max_blobs=int(g["B"].max()), state_dtype=pf.STATE_F64)
@@ -28,6 +29,7 @@ def test_engine_reproduces_fixture(name, bank):
     prm.rng_mode = int(g["rng_mode"])
     eng.set_params(prm)
     eng.set_option(pf.OPT_RECORD_COUNTS, 1)
+    eng.set_option(pf.OPT_FUSED, 1 if fused else 0)
     eng.set_prior(g["prior0"])
     nf = len(g["seed"])
     if bank:

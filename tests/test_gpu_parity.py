@@ -21,8 +21,9 @@ RNG = {"ref": pf.RNG_REFERENCE, "philox": pf.RNG_PHILOX}
 STATE = {"f64": pf.STATE_F64, "f32": pf.STATE_F32}
 
 
-def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None):
+def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None, fused=True):
     eng = pf.Engine(device=0, max_particles=max(N, 1), state_dtype=state)
+    eng.set_option(pf.OPT_FUSED, 1 if fused else 0)  # one cooperative launch per frame / two launches
     eng.set_model(markers, K, downgrade)
     prm = params or pf.default_params()
     prm.rng_mode = rng
@@ -78,12 +79,13 @@ CASES = [  # (N, M, B, heavy)
 @pytest.mark.parametrize("rng", ["ref", "philox"])
 @pytest.mark.parametrize("N,M,B,heavy", CASES)
 @pytest.mark.parametrize("prune", [True, False])
-def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune):
+@pytest.mark.parametrize("fused", [True, False])
+def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune, fused):
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 3)
     prm = pf.default_params()
     prm.rng_mode = RNG[rng]
-    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng], prune=prune)
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng], prune=prune, fused=fused)
     prior = st.prior()
     eng.set_prior(prior)
     for fr in st.frames:
@@ -96,7 +98,8 @@ def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune):
 
 
 @pytest.mark.parametrize("rng", ["ref", "philox"])
-def test_fp64_exit_rule_runs_all_iterations(rng):
+@pytest.mark.parametrize("fused", [True, False])
+def test_fp64_exit_rule_runs_all_iterations(rng, fused):
     """One LED occluded -> max weight < M*min(5,B): the loop runs all 80 iterations with noise growth
     and keeps the earliest strictly-best iteration (PE:606-624)."""
     N = 96
@@ -108,7 +111,7 @@ def test_fp64_exit_rule_runs_all_iterations(rng):
     blobs = np.vstack([true_px[1:], outliers]).astype(np.float32).astype(np.float64)
     prm = pf.default_params()
     prm.rng_mode = RNG[rng]
-    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng])
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng], fused=fused)
     prior = st.prior()
     eng.set_prior(prior)
     out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior, fr.current_pose, fr.predicted_pose,
@@ -120,12 +123,13 @@ def test_fp64_exit_rule_runs_all_iterations(rng):
 
 @pytest.mark.parametrize("state", ["f64", "f32"])
 @pytest.mark.parametrize("N", [1, 2, 3, 257])
-def test_small_particle_counts(state, N):
+@pytest.mark.parametrize("fused", [True, False])
+def test_small_particle_counts(state, N, fused):
     cfg = syn.StreamConfig("t", M=5, B=20, N=N)
     st = syn.make_stream(cfg, 2)
     prm = pf.default_params()
     prm.rng_mode = pf.RNG_REFERENCE
-    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_REFERENCE)
+    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_REFERENCE, fused=fused)
     prior = st.prior()
     eng.set_prior(prior)
     for fr in st.frames:
@@ -141,12 +145,13 @@ def test_small_particle_counts(state, N):
 
 
 @pytest.mark.parametrize("state", ["f64", "f32"])
-def test_no_blobs_reinitialises(state):
+@pytest.mark.parametrize("fused", [True, False])
+def test_no_blobs_reinitialises(state, fused):
     N = 300
     cfg = syn.StreamConfig("t", M=5, B=20, N=N)
     st = syn.make_stream(cfg, 1)
     fr = st.frames[0]
-    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX)
+    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX, fused=fused)
     prm = pf.default_params()
     eng.set_prior(st.prior())
     # B = 0: exit threshold M*min(5, B) = 0, so the reference stops after one iteration (PE:616)
@@ -380,3 +385,22 @@ def test_step_batch_matches_step_loop():
             assert x[k] == y[k]
         assert np.array_equal(x["winner_pose"], y["winner_pose"])
     assert np.array_equal(pa, pb)
+
+
+@pytest.mark.parametrize("rng", ["philox", "ref"])
+def test_fp64_exact_multi_group(rng):
+    """N = 140k: 547 blocks > one reduction group, so the 2-level hand-off tree (group waves + top wave,
+    carried group prefixes) runs; every discrete output must still match the oracle exactly."""
+    N = 140_000
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 1)
+    prm = pf.default_params()
+    prm.rng_mode = RNG[rng]
+    eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng])
+    prior = st.prior(fast=True)
+    eng.set_prior(prior)
+    fr = st.frames[0]
+    out, gpu, ref, arr = step_both(eng, prm, st.markers, st.K, prior, fr.current_pose, fr.predicted_pose,
+                                   fr.prediction, fr.blobs, seed=4242, frame_idx=fr.index)
+    assert_exact(out, gpu, ref, arr, N)
+    eng.close()
