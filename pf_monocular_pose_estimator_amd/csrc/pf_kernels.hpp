@@ -943,8 +943,9 @@ __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, c
 
 // group partial g of a weight slot: from memory, or (single-group frames) this iteration's values still
 // in registers
-__device__ __forceinline__ GroupPart group_part(const GroupPart* __restrict__ gp, int g, const GroupPart* regs) {
-  if (regs) return *regs;
+__device__ __forceinline__ GroupPart group_part(const GroupPart* __restrict__ gp, int g, const GroupPart& regs,
+                                                bool use_regs) {
+  if (use_regs) return regs;
   GroupPart r;
   r.sum = ld_wt_d(&gp[g].sum);
   r.zmax = ld_wt_d(&gp[g].zmax);
@@ -966,22 +967,35 @@ template <typename T, int RNG>
 __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __restrict__ ctrl, int iter,
                                               const GroupPart* __restrict__ gp0, const GroupPart* __restrict__ gp1,
                                               GroupScan* __restrict__ gscan, uint32_t* __restrict__ gen,
-                                              uint32_t gen_base, const GroupPart* cur) {
+                                              uint32_t gen_base, const GroupPart cur, bool have_cur, int slot) {
   const int lane = lane_id();
   const int ngrp = fa.ngrp;
+  // <= 64 groups: each lane's group partial of this iteration is loaded ONCE, in the same round trip as
+  // the control record, and serves every pass below
+  const bool one_tile = ngrp <= 64;
+  GroupPart q0;
+  q0.sum = 0.0;
+  q0.zmax = -INFINITY;
+  q0.zmin = INFINITY;
+  q0.maxw = -INFINITY;
+  q0.minw = INFINITY;
+  q0.argmax = q0.argmin = 0x7fffffff;
+  if (one_tile && lane < ngrp) q0 = group_part(slot ? gp1 : gp0, lane, cur, have_cur);
   const Ctrl c0 = load_ctrl_wt(ctrl);
-  const int slot = c0.cur_slot;
   // this iteration's max / first argmax
   double mv = -INFINITY;
   int mi = 0x7fffffff;
-  {
+  if (one_tile) {
+    mv = q0.maxw;
+    mi = q0.argmax;
+  } else {
     const GroupPart* P = slot ? gp1 : gp0;
     for (int g = lane; g < ngrp; g += 64) {
-      const GroupPart q = group_part(P, g, cur);
+      const GroupPart q = group_part(P, g, cur, have_cur);
       cmb_max(mv, mi, q.maxw, q.argmax);
     }
-    wave_argmax(mv, mi);
   }
+  wave_argmax(mv, mi);
   Ctrl c = c0;
   if (mv > c.best_max) {  // strict: PE:608
     c.best_max = mv;
@@ -999,13 +1013,17 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
     c.kept_slot = c.has_best ? c.best_slot : slot;
     c.kept_iter = c.has_best ? c.best_iter : iter;
     const GroupPart* KG = c.kept_slot ? gp1 : gp0;
-    const GroupPart* kreg = (c.kept_slot == slot) ? cur : nullptr;
+    const bool kreg = have_cur && c.kept_slot == slot;
+    // kept slot's partials of a one-tile frame: this iteration's (registers) or an earlier one's (load)
+    GroupPart kq = q0;
+    if (one_tile && c.kept_slot != slot && lane < ngrp) kq = group_part(KG, lane, cur, kreg);
+    auto kept_part = [&](int g) -> GroupPart { return one_tile ? kq : group_part(KG, g, cur, kreg); };
 
     // S = total over groups (tiles of 64 groups, carried)
     double carry = 0.0;
     for (int base = 0; base < ngrp; base += 64) {
       const int g = base + lane;
-      const double s = g < ngrp ? group_part(KG, g, kreg).sum : 0.0;
+      const double s = g < ngrp ? kept_part(g).sum : 0.0;
       carry = carry + lane_value(wave_incl_sum(s), 63);
     }
     const double S = carry;
@@ -1019,7 +1037,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
       q.sum = 0.0;
       q.zmax = -INFINITY;
       q.zmin = INFINITY;
-      if (g < ngrp) q = group_part(KG, g, kreg);
+      if (g < ngrp) q = kept_part(g);
       const double incl = wave_incl_sum(q.sum);
       const double prev = wave_shr1(incl, 0.0);
       const double G = lane == 0 ? carry : carry + prev;
@@ -1041,7 +1059,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
     double amv = -INFINITY, anv = INFINITY;
     int ami = 0x7fffffff, ani = 0x7fffffff;
     for (int g = lane; g < ngrp; g += 64) {
-      const GroupPart q = group_part(KG, g, kreg);
+      const GroupPart q = kept_part(g);
       cmb_max(amv, ami, q.maxw, q.argmax);
       cmb_min(anv, ani, q.minw, q.argmin);
     }
@@ -1159,7 +1177,7 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
   const bool single = fa.ngrp == 1;
   if (!single && !wave_arrive_last(tcount, fa.ngrp)) return;
   if (stamps && lane == 0) stamps[2] = rt_now();
-  propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, gen, gen_base, single ? &gr : nullptr);
+  propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, gen, gen_base, gr, single, slot);
   if (stamps && lane == 0) stamps[3] = rt_now();
 }
 
@@ -1205,92 +1223,110 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
                             ctrl, gcount, tcount, nullptr, 0u, stamps);
 }
 
-// ---- winner + frame record (one wave).  Writes into pinned host memory, then resets the control
-// record for the next frame.  Lanes 0-31 regenerate the most likely particle and lanes 32-63 the winner
-// in one pass; the winner's column minima run over blobs held one per lane (loaded once).
-template <typename T, int RNG, int MAXM>
-__device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
-                               const unsigned char* __restrict__ table, const T* __restrict__ prior, int winner,
-                               OutDev& rec, OutDev* __restrict__ out, int32_t tag, uint64_t* __restrict__ stamps) {
+// Winner candidate of one block: the block's first max-count particle, its kept pose and its
+// correspondences, published by the block's wave 1 (in parallel with wave 0's arrival) as data-tagged
+// granules: 8-byte words {payload (low 32 bits), frame sequence (high 32)}, each written by ONE
+// write-through store, so a reader that sees every tag current has every payload (MI355X_MICROARCH.md
+// "handoff-1to1").  Granules 0-23: the 12 pose doubles as lo/hi halves; 24-55: the 32 corr words;
+// 56: n_corr.  The global winner is one of these, so the final wave loads one block's granules.
+constexpr int kCandGran = 57;
+struct alignas(16) Cand {
+  uint64_t g[64];
+};
+
+// correspondences (PE:2385-2445 with pairs) of ONE pose P (uniform across the wave): blobs spread over
+// the lanes, (distance, original index) order as column_minima, then the sorting-network score.
+// Pairs go to corr (LDS), written by lane 0.
+template <typename T, int MAXM>
+__device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
+                                           const T* P, uint32_t* corr, int* np_out) {
   const int lane = lane_id();
   const int B = fa.B;
-  const LdsBlobs<T> tb = view_table<T>(table, B);  // global memory here
-  // table entries of this lane (chunk 0 covers B <= 64; larger B loops below)
-  T bx0 = (T)0, by0 = (T)0;
-  int o0 = 0x7fffffff;
-  if (lane < B) {
-    bx0 = tb.bx[lane];
-    by0 = tb.by[lane];
-    o0 = tb.orig[lane];
-  }
-  const int wsel = c.accepted ? winner : c.most_likely_idx;
-  T Q[12];
-  make_particle<T, RNG>(fa, sc, prior, lane < 32 ? c.most_likely_idx : wsel, c.kept_iter, Q);
-  T Pm[12], P[12];
+  T u[MAXM], v[MAXM], m[MAXM];
+  int r[MAXM];
+  project_markers<T, MAXM>(fa, sc, P, u, v);
+  T best[MAXM];
+  int arg[MAXM];
 #pragma unroll
-  for (int q = 0; q < 12; ++q) {
-    Pm[q] = lane_value(Q[q], 0);
-    P[q] = lane_value(Q[q], 32);
+  for (int j = 0; j < MAXM; ++j) {
+    best[j] = inf_t<T>();
+    arg[j] = 0x7fffffff;
   }
-  if (stamps && lane == 0) stamps[13] = stamps[14] = rt_now();
-  if (lane < 2 * kMaxMarkers) rec.corr[lane] = 0u;
-  wave_lds_sync();  // lane 0 writes the pairs over the cleared words below
+  for (int i = lane; i < B; i += 64) {
+    const T bx = tb.bx[i], by = tb.by[i];
+    const int o = tb.orig[i];
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      const T dx = bx - u[j];
+      const T dy = by - v[j];
+      const T d = fmadd(dx, dx, dy * dy);
+      if (d < best[j] || (d == best[j] && o < arg[j])) {
+        best[j] = d;
+        arg[j] = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    if (j < fa.M) wave_argmin(best[j], arg[j]);  // uniform branch
+    m[j] = best[j];
+    r[j] = arg[j] == 0x7fffffff ? 0 : arg[j];
+  }
+  if (lane < 2 * kMaxMarkers) corr[lane] = 0u;
+  wave_lds_sync();  // lane 0 writes the pairs over the cleared words
   int np = 0;
+  if (lane == 0 && B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0]))
+    score_minima<T, MAXM, true>(fa, m, r, corr, &np);
+  *np_out = lane_value(np, 0);
+  wave_lds_sync();
+}
+
+// ---- frame record (one wave) into pinned host memory: the scalars from the control record, the
+// winner's pose and pairs from its block's candidate record, the most likely pose from `mlpose`; then
+// the tag release and the reset of the control record for the next frame.  On the re-init branch
+// (winner < 0) the most likely particle is regenerated here and there are no pairs.
+template <typename T, int RNG, int MAXM>
+__device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c,
+                                               Ctrl* __restrict__ ctrl, const T* __restrict__ prior, int winner,
+                                               const Cand* __restrict__ cand, const double* __restrict__ mlpose,
+                                               OutDev& rec, OutDev* __restrict__ out, int32_t tag,
+                                               uint64_t* __restrict__ stamps) {
+  const int lane = lane_id();
   if (c.accepted) {
-    T u[MAXM], v[MAXM], m[MAXM];
-    int r[MAXM];
-    project_markers<T, MAXM>(fa, sc, P, u, v);
-    T best[MAXM];
-    int arg[MAXM];
-#pragma unroll
-    for (int j = 0; j < MAXM; ++j) {
-      best[j] = inf_t<T>();
-      arg[j] = 0x7fffffff;
+    // the winner's candidate granules (one round trip; re-polled, bounded, while a tag is stale) and the
+    // most likely pose
+    const Cand* wc = cand + winner / kBlock;
+    double ml = 0.0;
+    if (lane < 12) ml = ld_wt_d(mlpose + lane);
+    uint64_t gv = 0;
+    const uint64_t t0 = rt_now();
+    for (;;) {
+      if (lane < kCandGran) gv = ld_wt(&wc->g[lane]);
+      const bool stale = lane < kCandGran && (uint32_t)(gv >> 32) != (uint32_t)(tag >> 1);
+      if (!__builtin_amdgcn_ballot_w64(stale)) break;
+      if (rt_now() - t0 > 200000000ull) return;  // 2 s: abandon (no record; the host reports it)
+      __builtin_amdgcn_s_sleep(1);
     }
-    // (distance, original index) order, as column_minima
-    for (int base = 0; base < B; base += 64) {
-      const int i = base + lane;
-      T bx = bx0, by = by0;
-      int o = o0;
-      if (base > 0 && i < B) {
-        bx = tb.bx[i];
-        by = tb.by[i];
-        o = tb.orig[i];
-      }
-      if (i < B) {
+    const uint32_t pl = (uint32_t)gv;
+    uint32_t* wp = (uint32_t*)rec.winner_pose;
+    if (lane < 24) wp[lane] = pl;  // little-endian halves of the 12 doubles
+    if (lane >= 24 && lane < 24 + 2 * kMaxMarkers) rec.corr[lane - 24] = pl;
+    if (lane == 56) rec.n_corr = (int32_t)pl;
+    if (lane < 12) rec.most_likely_pose[lane] = ml;
+  } else {
+    T Q[12];
+    make_particle<T, RNG>(fa, sc, prior, c.most_likely_idx, c.kept_iter, Q);
+    if (lane < 12) {  // lane q writes pose word q (selects, no dynamic register indexing)
+      T pm = Q[0];
 #pragma unroll
-        for (int j = 0; j < MAXM; ++j) {
-          const T dx = bx - u[j];
-          const T dy = by - v[j];
-          const T d = fmadd(dx, dx, dy * dy);
-          if (d < best[j] || (d == best[j] && o < arg[j])) {
-            best[j] = d;
-            arg[j] = o;
-          }
-        }
-      }
+      for (int q = 1; q < 12; ++q) pm = lane == q ? Q[q] : pm;
+      rec.most_likely_pose[lane] = (double)pm;
+      rec.winner_pose[lane] = (double)pm;
     }
-#pragma unroll
-    for (int j = 0; j < MAXM; ++j) {
-      if (j < fa.M) wave_argmin(best[j], arg[j]);  // uniform branch
-      m[j] = best[j];
-      r[j] = arg[j] == 0x7fffffff ? 0 : arg[j];
-    }
-    if (stamps && lane == 0) stamps[15] = rt_now();
-    if (lane == 0 && B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0]))
-      score_minima<T, MAXM, true>(fa, m, r, rec.corr, &np);  // pairs straight into the LDS record
-    if (stamps && lane == 0) stamps[16] = rt_now();
+    if (lane < 2 * kMaxMarkers) rec.corr[lane] = 0u;
+    if (lane == 0) rec.n_corr = 0;
   }
-  if (lane < 12) {  // lane q writes pose word q (selects, no dynamic register indexing)
-    T pm = Pm[0], pw = P[0];
-#pragma unroll
-    for (int q = 1; q < 12; ++q) {
-      pm = lane == q ? Pm[q] : pm;
-      pw = lane == q ? P[q] : pw;
-    }
-    rec.most_likely_pose[lane] = (double)pm;
-    rec.winner_pose[lane] = (double)pw;
-  }
+  if (stamps && lane == 0) stamps[13] = stamps[14] = stamps[15] = stamps[16] = rt_now();
   if (lane == 0) {
     rec.kept_slot = c.kept_slot;
     rec.iters = c.iters;
@@ -1302,7 +1338,6 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
     rec.flag_fail = c.accepted ? 1 : 4;
     rec.highest_prob = c.has_best ? c.best_max : 0.0;
     rec.prob_sum = c.S;
-    rec.n_corr = np;
     if (stamps) stamps[17] = rt_now();
   }
   wave_lds_sync();
@@ -1323,6 +1358,7 @@ template <typename T>
 struct ResampleLds {
   double sum[kWaves], max[kWaves];
   int hi[kWaves], c[kWaves], ci[kWaves];
+  uint32_t ccorr[2 * kMaxMarkers];  // wave 1's pair scratch for the block candidate
   struct alignas(16) Row {
     T q[12];
   } rows[kWaves][64];
@@ -1337,6 +1373,7 @@ __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ post, double wd, const T* A,
     const T* P_in, bool have_P, const BlockScan& bs, const GroupScan& gs, ResampleLds<T>& sh, OutDev& rec,
+    const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq,
     uint64_t* __restrict__ stamps) {
@@ -1411,6 +1448,15 @@ __device__ __forceinline__ void resample_phase(
 #pragma unroll
   for (int q = 0; q < 12; ++q) P[q] = have_P ? P_in[q] : (T)0;
   if (!have_P && e > a) propagate<T, RNG>(fa, sc, A, n, kiter, P);
+  if (valid && n == c.most_likely_idx) {  // the most likely pose for the frame record (write-through)
+    T Q[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) Q[q] = P[q];
+    if (!have_P && !(e > a)) propagate<T, RNG>(fa, sc, A, n, kiter, Q);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) st_wt_d(mlpose + q, (double)Q[q]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the block barrier / arrival
+  }
 
   // Wave-cooperative scatter.  The wave's lanes own consecutive slot ranges [a, e) (empty lanes have
   // a = e = the next start), so slot k belongs to the highest non-empty lane whose start is <= k.  Per
@@ -1418,11 +1464,11 @@ __device__ __forceinline__ void resample_phase(
   // across chunks) fills every slot's owner, and the slot lane reads the owner's row from LDS.
   const int wa = lane_value(a, 0);
   const int we = lane_value(e, 63);
-  if (we > wa) {
-    auto& rows = sh.rows[wv];
-    int* map = sh.map[wv];
+  auto& rows = sh.rows[wv];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];
+  for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];  // also read by wave 0 for the block candidate
+  if (we > wa) {
+    int* map = sh.map[wv];
     int carry = -1;
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 21, rt_now());
     for (int base = wa; base < we; base += 64) {
@@ -1447,7 +1493,40 @@ __device__ __forceinline__ void resample_phase(
 
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 12, rt_now());
   __syncthreads();
+  if (wv == 1) {  // this block's winner candidate, in parallel with wave 0's arrival
+    int cbv = sh.c[0], cbi = sh.ci[0];
+    for (int w = 1; w < kWaves; ++w) cmb_max(cbv, cbi, sh.c[w], sh.ci[w]);
+    // a candidate with copies was propagated by its lane (staged rows); with no copies anywhere in the
+    // block (only possible when every count of the frame is 0: the winner is particle 0, PE:685) it is
+    // regenerated here
+    const int loc = cbi - blk * kBlock;
+    T Pc[12];
+    if (cbv > 0) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) Pc[q] = sh.rows[loc >> 6][loc & 63].q[q];
+    } else {
+      make_particle<T, RNG>(fa, sc, prior, cbi, kiter, Pc);
+    }
+    int np = 0;
+    pose_pairs<T, MAXM>(fa, sc, tb, Pc, sh.ccorr, &np);
+    uint32_t pl = 0;
+    if (lane < 24) {
+      T pv = Pc[0];
+#pragma unroll
+      for (int q = 1; q < 12; ++q) pv = (lane >> 1) == q ? Pc[q] : pv;
+      const uint64_t bits = (uint64_t)__double_as_longlong((double)pv);
+      pl = (lane & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+    } else if (lane < 24 + 2 * kMaxMarkers) {
+      pl = sh.ccorr[lane - 24];
+    } else if (lane == 56) {
+      pl = (uint32_t)np;
+    }
+    if (lane < kCandGran) st_wt(&cand[blk].g[lane], ((uint64_t)(uint32_t)seq << 32) | pl);
+    if (stamps && lane == 0) stamp_max(stamps, 22, rt_now());
+    return;
+  }
   if (wv != 0) return;
+
   int last = 0;
   if (lane == 0) {
     int bv = sh.c[0], bi = sh.ci[0];
@@ -1480,7 +1559,7 @@ __device__ __forceinline__ void resample_phase(
   }
   if (stamps && lane == 0) stamps[6] = rt_now();
   // winner = argmax resample count, first index (PE:685-686)
-  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, bi, rec, out, 2 * seq + 1, stamps);
+  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, bi, cand, mlpose, rec, out, 2 * seq + 1, stamps);
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
@@ -1491,7 +1570,8 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
-    uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, OutDev* __restrict__ out,
+    int32_t seq, uint64_t* __restrict__ stamps) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
@@ -1521,15 +1601,16 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
     if (blockIdx.x == 0 && threadIdx.x < 64) {
       wave_lds_sync();
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
     }
     return;
   }
   const int slot = c.kept_slot;
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
-  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec,
-                               cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+  const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
+  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
+                               mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
 }
 
 // ---- the whole frame in ONE cooperative launch (every block co-resident, checked by the host): the
@@ -1553,6 +1634,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
     Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup,
     uint32_t* __restrict__ gcount_w, uint32_t* __restrict__ tcount_w, uint32_t* __restrict__ gcount_r,
     uint32_t* __restrict__ tcount_r, uint32_t* __restrict__ gen, uint32_t* __restrict__ counts,
+    Cand* __restrict__ cand, double* __restrict__ mlpose,
     OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
@@ -1637,7 +1719,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
 
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
     if (blk == 0 && wv == 0)
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, -1, rec, out, 2 * seq + 1, stamps);
+      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
     return;
   }
   const int kslot = c.kept_slot;
@@ -1652,8 +1734,8 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   }
   const BlockScan bs = fsh.bs[kslot];
   const GroupScan gs = fsh.gs;
-  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, cpart,
-                               cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
+  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+                               mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path)

@@ -54,6 +54,8 @@ struct pfmpe_ctx {
   CountPart* d_cgroup = nullptr;
   uint32_t* d_counters = nullptr;  // [prop group x max_grp][prop top][res group x max_grp][res top]
   uint32_t* d_gen = nullptr;       // k_frame iteration release word (monotonic)
+  Cand* d_cand = nullptr;          // per-block winner candidates
+  double* d_mlpose = nullptr;      // most likely pose (12)
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
   bool fused = true;               // PFMPE_OPT_FUSED
@@ -232,7 +234,8 @@ struct Seq {
       hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
-                         c->record_counts ? c->d_counts : nullptr, c->d_out, seq, c->d_stamps);
+                         c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
+                         c->d_stamps);
     }));
     RET(wait_frame(c));
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
@@ -273,7 +276,8 @@ struct Seq {
       hipLaunchKernelGGL((k_frame<T, RNG, MAXM, PRUNE>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, a, table,
                          prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
-                         tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_out, seq, c->d_stamps);
+                         tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
+                         c->d_stamps);
     }));
     *launched = true;
     if (wait_frame(c) != PFMPE_OK) {
