@@ -336,9 +336,11 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
 template <typename T, int RNG>
 int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
   const FrameArgsT<T> fa = build_args<T>(c, in);
-  // marker capacity buckets: the per-particle loops are unrolled to MAXM (5: the 5-LED configs C1/C2/C4)
+  // marker capacity buckets: the per-particle loops are unrolled to MAXM (5: the 5-LED configs C1/C2/C4,
+  // 12: C3)
   if (fa.M <= 5) return Seq<T, RNG, 5>::step(c, fa, table);
   if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, table);
+  if (fa.M <= 12) return Seq<T, RNG, 12>::step(c, fa, table);
   return Seq<T, RNG, 16>::step(c, fa, table);
 }
 
