@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--particles", type=int, default=0, help="override N")
     ap.add_argument("--force-iters", type=int, default=0)
     ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
+    ap.add_argument("--state", default="", choices=["", "f32", "f16", "f64"],
+                    help="particle state storage (default: f16 for C4 per BASELINE.json configs[3], else f32)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--timing-period", type=int, default=25,
@@ -129,7 +131,9 @@ def main():
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=args.particles or base.N, heavy=base.heavy, seed=rank)
     n_frames = args.warmup + args.steps
     st = syn.make_stream(cfg, n_frames)
-    eng = pf.Engine(device=local_rank, max_particles=cfg.N, state_dtype=pf.STATE_F32)
+    state = args.state or ("f16" if cfg.name == "C4" else "f32")
+    state_dtype = {"f32": pf.STATE_F32, "f16": pf.STATE_F16, "f64": pf.STATE_F64}[state]
+    eng = pf.Engine(device=local_rank, max_particles=cfg.N, state_dtype=state_dtype)
     eng.set_model(st.markers, st.K)
     prm = pf.default_params()
     prm.rng_mode = pf.RNG_PHILOX if args.rng == "philox" else pf.RNG_REFERENCE
@@ -168,7 +172,7 @@ def main():
     elapsed, total_updates = combine_ranks(dist, elapsed, updates)
 
     if rank == 0:
-        S = 48  # fp32 SoA state bytes per particle
+        S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
         ab = algorithmic_bytes(S, cfg.N)
         roof = None
         timed = {k: v for k, v in stats.items() if v[0] > 0}
@@ -199,11 +203,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if state != "f64" else "f64",
             "data": "synthetic",
             "config": {
-                "workload": f"{cfg.name}: {cfg.M} LEDs, {cfg.N} particles, {cfg.B} blobs/frame, fp32 SoA state "
-                            f"(BASELINE.json configs[1])" if cfg.name == "C2" else f"{cfg.name}",
+                "workload": f"{cfg.name}: {cfg.M} LEDs, {cfg.N} particles, {cfg.B} blobs/frame"
+                            f"{' (heavy outliers)' if cfg.heavy else ''}, {state} SoA state"
+                            + (" (BASELINE.json configs[1])" if cfg.name == "C2" else ""),
+                "state": state,
                 "N_particles": cfg.N, "markers": cfg.M, "blobs": cfg.B,
                 "frames_per_sec_per_gpu": args.steps / elapsed,
                 "iters_per_frame": k_mean, "accept_rate": accepted / max(1, args.steps),

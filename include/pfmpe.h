@@ -40,8 +40,10 @@ enum {
   PFMPE_E_STATE = -4  /* call order (e.g. step before set_model)    */
 };
 
-/* particle state storage in HBM (SoA planes) */
-enum { PFMPE_STATE_F32 = 0, PFMPE_STATE_F64 = 1 };
+/* particle state storage in HBM (SoA planes).  F16: fp16 deltas to an anchor pose per particle set
+ * (the frame's current pose for a resampled set, the first particle for pfmpe_set_prior), fp32 compute
+ * and fp32 weights: 24 B per particle (BASELINE.json configs[3]). */
+enum { PFMPE_STATE_F32 = 0, PFMPE_STATE_F64 = 1, PFMPE_STATE_F16 = 2 };
 
 /* motion / resample random streams */
 enum {

@@ -690,11 +690,12 @@ static bool ldlt_solve6(const double A_in[36], const double b_in[6], double x[6]
     }
     const double d = A[k * 6 + k];
     if (d == 0) return false;
-    for (int i = k + 1; i < 6; ++i) {
-      const double l = A[i * 6 + k] / d;
-      for (int j = k + 1; j <= i; ++j) A[i * 6 + j] -= l * A[j * 6 + k];
-      A[i * 6 + k] = l;
-    }
+    double l[6] = {0};
+    for (int i = k + 1; i < 6; ++i) l[i] = A[i * 6 + k] / d;
+    // Schur update with the ORIGINAL column k (multipliers are stored only afterwards)
+    for (int i = k + 1; i < 6; ++i)
+      for (int j = k + 1; j <= i; ++j) A[i * 6 + j] -= l[i] * A[j * 6 + k];
+    for (int i = k + 1; i < 6; ++i) A[i * 6 + k] = l[i];
     for (int i = k + 1; i < 6; ++i)
       for (int j = i + 1; j < 6; ++j) A[i * 6 + j] = A[j * 6 + i];
   }

@@ -17,7 +17,7 @@ MAX_MARKERS = 16
 MAX_BLOBS = 1024
 
 OK, E_ARG, E_HIP, E_CAP, E_STATE = 0, -1, -2, -3, -4
-STATE_F32, STATE_F64 = 0, 1
+STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4

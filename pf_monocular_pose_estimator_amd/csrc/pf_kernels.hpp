@@ -33,6 +33,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_fp16.h>
+
 #include "pf_rng.hpp"
 
 namespace pfmpe {
@@ -72,6 +74,7 @@ struct FrameArgsT {
   int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
   int32_t diag, pad_;             // diagnostic switches (0 in production)
   int64_t ld;                     // SoA plane stride in elements
+  T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
 };
 
 // The frame-constant arrays, staged once per block into LDS and read from there (broadcast reads):
@@ -211,11 +214,24 @@ __device__ __forceinline__ void compose(const T* A, const T* B, T* C) {
   }
 }
 
+// Particle state storage S for compute type T: S == T (fp32 / fp64 planes), or fp16 planes holding
+// deltas to the set's anchor pose (PFMPE_STATE_F16, fp32 compute): 24 B per particle.
+template <typename T, typename SP>
+struct StateIO {
+  static __device__ __forceinline__ T load(SP v, T) { return (T)v; }
+  static __device__ __forceinline__ SP store(T v, T) { return (SP)v; }
+};
+template <>
+struct StateIO<float, __half> {
+  static __device__ __forceinline__ float load(__half v, float anchor) { return __half2float(v) + anchor; }
+  static __device__ __forceinline__ __half store(float v, float anchor) { return __float2half(v - anchor); }
+};
+
 // prior particle n (SoA planes), loaded ahead of use so the loads overlap other work
-template <typename T>
-__device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const T* __restrict__ prior, int n, T* A) {
+template <typename T, typename SP>
+__device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __restrict__ prior, int n, T* A) {
 #pragma unroll
-  for (int q = 0; q < 12; ++q) A[q] = prior[(int64_t)q * fa.ld + n];
+  for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(prior[(int64_t)q * fa.ld + n], fa.anc_in[q]);
 }
 
 // The motion model (PE:543-588) for particle n in PF iteration `iter` from its prior pose A (loaded by
@@ -294,9 +310,9 @@ __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsCons
   }
 }
 
-template <typename T, int RNG>
+template <typename T, int RNG, typename SP>
 __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc,
-                                              const T* __restrict__ prior, int n, int iter, T* P) {
+                                              const SP* __restrict__ prior, int n, int iter, T* P) {
   T A[12];
   if (n >= 2) load_prior(fa, prior, n, A);
   propagate<T, RNG>(fa, sc, A, n, iter, P);
@@ -1182,9 +1198,9 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
 }
 
 // ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread
-template <typename T, int RNG, int MAXM, bool PRUNE>
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
-    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ w0,
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior, T* __restrict__ w0,
     T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
     BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
     GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
@@ -1285,9 +1301,9 @@ __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsCon
 // winner's pose and pairs from its block's candidate record, the most likely pose from `mlpose`; then
 // the tag release and the reset of the control record for the next frame.  On the re-init branch
 // (winner < 0) the most likely particle is regenerated here and there are no pairs.
-template <typename T, int RNG, int MAXM>
+template <typename T, int RNG, int MAXM, typename SP>
 __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c,
-                                               Ctrl* __restrict__ ctrl, const T* __restrict__ prior, int winner,
+                                               Ctrl* __restrict__ ctrl, const SP* __restrict__ prior, int winner,
                                                const Cand* __restrict__ cand, const double* __restrict__ mlpose,
                                                OutDev& rec, OutDev* __restrict__ out, int32_t tag,
                                                uint64_t* __restrict__ stamps) {
@@ -1315,7 +1331,7 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
     if (lane < 12) rec.most_likely_pose[lane] = ml;
   } else {
     T Q[12];
-    make_particle<T, RNG>(fa, sc, prior, c.most_likely_idx, c.kept_iter, Q);
+    make_particle<T, RNG, SP>(fa, sc, prior, c.most_likely_idx, c.kept_iter, Q);
     if (lane < 12) {  // lane q writes pose word q (selects, no dynamic register indexing)
       T pm = Q[0];
 #pragma unroll
@@ -1368,10 +1384,10 @@ struct ResampleLds {
 // ---- stratified resampling of one block (PE:666-682) + count partials -> winner -> frame record.
 // wd: the thread's kept raw weight (0 for invalid lanes); P: its kept propagated particle when have_P,
 // else regenerated here from A (P_in unused).  Called by every thread; the caller checked c.done && c.accepted.
-template <typename T, int RNG, int MAXM>
+template <typename T, int RNG, int MAXM, typename SP>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
-    const unsigned char* __restrict__ table, const T* __restrict__ prior, T* __restrict__ post, double wd, const T* A,
+    const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
     const T* P_in, bool have_P, const BlockScan& bs, const GroupScan& gs, ResampleLds<T>& sh, OutDev& rec,
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
@@ -1486,7 +1502,7 @@ __device__ __forceinline__ void resample_phase(
       if (k < we) {
         const auto& row = rows[own];
 #pragma unroll
-        for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = row.q[q];
+        for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
       }
     }
   }
@@ -1505,7 +1521,7 @@ __device__ __forceinline__ void resample_phase(
 #pragma unroll
       for (int q = 0; q < 12; ++q) Pc[q] = sh.rows[loc >> 6][loc & 63].q[q];
     } else {
-      make_particle<T, RNG>(fa, sc, prior, cbi, kiter, Pc);
+      make_particle<T, RNG, SP>(fa, sc, prior, cbi, kiter, Pc);
     }
     int np = 0;
     pose_pairs<T, MAXM>(fa, sc, tb, Pc, sh.ccorr, &np);
@@ -1559,15 +1575,15 @@ __device__ __forceinline__ void resample_phase(
   }
   if (stamps && lane == 0) stamps[6] = rt_now();
   // winner = argmax resample count, first index (PE:685-686)
-  finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, bi, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+  finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, bi, cand, mlpose, rec, out, 2 * seq + 1, stamps);
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
 // ---- launch 2 of the two-launch path: stratified resampling + winner + frame record
-template <typename T, int RNG, int MAXM>
+template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kBlock) void k_resample(
-    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const T* __restrict__ prior,
-    T* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, OutDev* __restrict__ out,
@@ -1601,7 +1617,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
     if (blockIdx.x == 0 && threadIdx.x < 64) {
       wave_lds_sync();
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+      finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
     }
     return;
   }
@@ -1609,7 +1625,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
-  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
+  resample_phase<T, RNG, MAXM, SP>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
                                mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
 }
 
@@ -1625,10 +1641,10 @@ struct FrameLds {
   int abort;
 };
 
-template <typename T, int RNG, int MAXM, bool PRUNE>
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) void k_frame(
-    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const T* __restrict__ prior,
-    T* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
     BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1,
     GroupPart* __restrict__ gpart0, GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
     Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup,
@@ -1719,7 +1735,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
 
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
     if (blk == 0 && wv == 0)
-      finalize_frame<T, RNG, MAXM>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+      finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
     return;
   }
   const int kslot = c.kept_slot;
@@ -1734,25 +1750,34 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   }
   const BlockScan bs = fsh.bs[kslot];
   const GroupScan gs = fsh.gs;
-  resample_phase<T, RNG, MAXM>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+  resample_phase<T, RNG, MAXM, SP>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
                                mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
 }
 
-// ---- state import / export / regeneration (API helpers, not on the timed path)
+// ---- state import / export / regeneration (API helpers, not on the timed path).  anchor: the set's
+// anchor pose (fp16 state), ignored for fp32 / fp64 planes.
 template <typename T>
-__global__ void k_import(const double* __restrict__ poses, T* __restrict__ st, int N, int64_t ld) {
+struct Pose12 {
+  T v[12];
+};
+template <typename T, typename SP>
+__global__ void k_import(const double* __restrict__ poses, SP* __restrict__ st, int N, int64_t ld,
+                         const Pose12<T> anchor) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  for (int q = 0; q < 12; ++q) st[(int64_t)q * ld + n] = (T)poses[12 * (int64_t)n + q];
+  for (int q = 0; q < 12; ++q)
+    st[(int64_t)q * ld + n] = StateIO<T, SP>::store((T)poses[12 * (int64_t)n + q], anchor.v[q]);
 }
-template <typename T>
-__global__ void k_export(const T* __restrict__ st, double* __restrict__ poses, int N, int64_t ld) {
+template <typename T, typename SP>
+__global__ void k_export(const SP* __restrict__ st, double* __restrict__ poses, int N, int64_t ld,
+                         const Pose12<T> anchor) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)st[(int64_t)q * ld + n];
+  for (int q = 0; q < 12; ++q)
+    poses[12 * (int64_t)n + q] = (double)StateIO<T, SP>::load(st[(int64_t)q * ld + n], anchor.v[q]);
 }
-template <typename T, int RNG>
-__global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int kept_iter, const T* __restrict__ prior,
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int kept_iter, const SP* __restrict__ prior,
                                                  double* __restrict__ poses) {
   __shared__ LdsConst<T> sc;
   stage_consts(fa, sc);
@@ -1760,7 +1785,7 @@ __global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int ke
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= fa.N) return;
   T P[12];
-  make_particle<T, RNG>(fa, sc, prior, n, kept_iter, P);
+  make_particle<T, RNG, SP>(fa, sc, prior, n, kept_iter, P);
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)P[q];
 }
 template <typename T>

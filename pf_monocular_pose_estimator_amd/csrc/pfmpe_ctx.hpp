@@ -38,7 +38,9 @@ struct pfmpe_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int max_particles = 0, max_markers = 0, max_blobs = 0, state_dtype = PFMPE_STATE_F32;
-  size_t es = 4;       // bytes per state element
+  size_t es = 4;       // bytes per state element (4 fp32, 8 fp64, 2 fp16 deltas)
+  size_t ws = 4;       // bytes per weight (compute type)
+  double anchor[2][12] = {{0}};  // fp16 state: anchor pose of each state buffer
   int64_t ld = 0;      // plane stride (elements)
   int max_blk = 0;
 
@@ -203,35 +205,35 @@ template <typename T> FrameArgsT<T>& last_args(pfmpe_ctx* c);
 template <> inline FrameArgsT<float>& last_args<float>(pfmpe_ctx* c) { return c->last_fa_f; }
 template <> inline FrameArgsT<double>& last_args<double>(pfmpe_ctx* c) { return c->last_fa_d; }
 
-template <typename T, int RNG, int MAXM>
+template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
   static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, int iter) {
-    const T* prior = (const T*)c->d_state[c->prior_idx];
+    const SP* prior = (const SP*)c->d_state[c->prior_idx];
     const size_t lds = BlobTable<T>::bytes(fa.B);
     uint32_t* gcount = c->d_counters;
     uint32_t* tcount = c->d_counters + c->max_grp;
     return launch(c, PFMPE_K_PROPAGATE, [&] {
       if (c->prune)
-        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
                            table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
                            c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
                            c->d_stamps);
       else
-        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
+        hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
                            table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
                            c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
                            c->d_stamps);
     });
   }
   static int finish(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
-    const T* prior = (const T*)c->d_state[c->prior_idx];
-    T* post = (T*)c->d_state[1 - c->prior_idx];
+    const SP* prior = (const SP*)c->d_state[c->prior_idx];
+    SP* post = (SP*)c->d_state[1 - c->prior_idx];
     uint32_t* gcount = c->d_counters + c->max_grp + 1;
     uint32_t* tcount = c->d_counters + 2 * c->max_grp + 1;
     c->seq = (c->seq + 1) & 0x3fffffff;
     const int32_t seq = c->seq;
     RET(launch(c, PFMPE_K_RESAMPLE, [&] {
-      hipLaunchKernelGGL((k_resample<T, RNG, MAXM>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, table,
+      hipLaunchKernelGGL((k_resample<T, RNG, MAXM, SP>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
@@ -245,7 +247,7 @@ struct Seq {
   template <bool PRUNE>
   static int frame_fused(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, bool* launched) {
     *launched = false;
-    const void* fn = (const void*)k_frame<T, RNG, MAXM, PRUNE>;
+    const void* fn = (const void*)k_frame<T, RNG, MAXM, PRUNE, SP>;
     const size_t lds = BlobTable<T>::bytes(fa.B);
     auto key = std::make_pair(fn, lds);
     auto it = c->occ.find(key);
@@ -260,8 +262,8 @@ struct Seq {
     // "coop-launch"); every in-kernel wait is bounded anyway.
     const int per_cu = std::min(2, it->second - 1);
     if (per_cu < 1 || (int64_t)per_cu * c->num_cu < fa.nblk) return PFMPE_OK;  // two-launch path
-    const T* prior = (const T*)c->d_state[c->prior_idx];
-    T* post = (T*)c->d_state[1 - c->prior_idx];
+    const SP* prior = (const SP*)c->d_state[c->prior_idx];
+    SP* post = (SP*)c->d_state[1 - c->prior_idx];
     T* w0 = (T*)c->d_w[0];
     T* w1 = (T*)c->d_w[1];
     uint32_t* gcount_w = c->d_counters;
@@ -273,7 +275,7 @@ struct Seq {
     int32_t seq = c->seq;
     const FrameArgsT<T> a = fa;
     RET(launch(c, PFMPE_K_FRAME, [&] {
-      hipLaunchKernelGGL((k_frame<T, RNG, MAXM, PRUNE>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, a, table,
+      hipLaunchKernelGGL((k_frame<T, RNG, MAXM, PRUNE, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, a, table,
                          prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
                          tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
@@ -324,8 +326,8 @@ struct Seq {
   static int regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
     const FrameArgsT<T>& fa = last_args<T>(c);
     return launch(c, PFMPE_K_AUX, [&] {
-      hipLaunchKernelGGL((k_regen<T, RNG>), dim3((fa.N + 255) / 256), dim3(256), 0, c->stream, fa, kept_iter,
-                         (const T*)prior, out);
+      hipLaunchKernelGGL((k_regen<T, RNG, SP>), dim3((fa.N + 255) / 256), dim3(256), 0, c->stream, fa, kept_iter,
+                         (const SP*)prior, out);
     });
   }
 };
@@ -333,20 +335,24 @@ struct Seq {
 template <typename T>
 FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
 
-template <typename T, int RNG>
+template <typename T, int RNG, typename SP>
 int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
-  const FrameArgsT<T> fa = build_args<T>(c, in);
+  FrameArgsT<T> fa = build_args<T>(c, in);
+  for (int q = 0; q < 12; ++q) {  // fp16 state: anchors of the prior and of the new prior (current pose)
+    fa.anc_in[q] = (T)c->anchor[c->prior_idx][q];
+    fa.anc_out[q] = (T)in->current_pose[q];
+  }
   // marker capacity buckets: the per-particle loops are unrolled to MAXM (5: the 5-LED configs C1/C2/C4,
   // 12: C3)
-  if (fa.M <= 5) return Seq<T, RNG, 5>::step(c, fa, table);
-  if (fa.M <= 8) return Seq<T, RNG, 8>::step(c, fa, table);
-  if (fa.M <= 12) return Seq<T, RNG, 12>::step(c, fa, table);
-  return Seq<T, RNG, 16>::step(c, fa, table);
+  if (fa.M <= 5) return Seq<T, RNG, 5, SP>::step(c, fa, table);
+  if (fa.M <= 8) return Seq<T, RNG, 8, SP>::step(c, fa, table);
+  if (fa.M <= 12) return Seq<T, RNG, 12, SP>::step(c, fa, table);
+  return Seq<T, RNG, 16, SP>::step(c, fa, table);
 }
 
-template <typename T, int RNG>
+template <typename T, int RNG, typename SP>
 int regen_m(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
-  return Seq<T, RNG, 8>::regen(c, kept_iter, prior, out);
+  return Seq<T, RNG, 8, SP>::regen(c, kept_iter, prior, out);
 }
 
 inline bool is_identity12(const double* p) {
@@ -418,8 +424,8 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
 }
 
 
-#define PFMPE_DECLARE_INSTANCE(T, RNG, EXT)                                                              \
-  EXT template int dispatch_m<T, RNG>(pfmpe_ctx*, const pfmpe_frame_in*, const unsigned char*);           \
-  EXT template int regen_m<T, RNG>(pfmpe_ctx*, int, const void*, double*);
+#define PFMPE_DECLARE_INSTANCE(T, RNG, SP, EXT)                                                           \
+  EXT template int dispatch_m<T, RNG, SP>(pfmpe_ctx*, const pfmpe_frame_in*, const unsigned char*);        \
+  EXT template int regen_m<T, RNG, SP>(pfmpe_ctx*, int, const void*, double*);
 
 }  // namespace pfmpe_impl

@@ -9,29 +9,61 @@ using namespace pfmpe;
 using namespace pfmpe_impl;
 
 namespace pfmpe_impl {
-PFMPE_DECLARE_INSTANCE(float, kRngReference, extern)
-PFMPE_DECLARE_INSTANCE(float, kRngPhilox, extern)
-PFMPE_DECLARE_INSTANCE(double, kRngReference, extern)
-PFMPE_DECLARE_INSTANCE(double, kRngPhilox, extern)
+PFMPE_DECLARE_INSTANCE(float, kRngReference, float, extern)
+PFMPE_DECLARE_INSTANCE(float, kRngPhilox, float, extern)
+PFMPE_DECLARE_INSTANCE(double, kRngReference, double, extern)
+PFMPE_DECLARE_INSTANCE(double, kRngPhilox, double, extern)
+PFMPE_DECLARE_INSTANCE(float, kRngReference, __half, extern)
+PFMPE_DECLARE_INSTANCE(float, kRngPhilox, __half, extern)
 }  // namespace pfmpe_impl
 
 namespace {
 using namespace pfmpe_impl;
 
 int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
-  const bool f64 = c->state_dtype == PFMPE_STATE_F64;
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
-  if (f64) return ref ? dispatch_m<double, kRngReference>(c, in, table) : dispatch_m<double, kRngPhilox>(c, in, table);
-  return ref ? dispatch_m<float, kRngReference>(c, in, table) : dispatch_m<float, kRngPhilox>(c, in, table);
+  switch (c->state_dtype) {
+    case PFMPE_STATE_F64:
+      return ref ? dispatch_m<double, kRngReference, double>(c, in, table)
+                 : dispatch_m<double, kRngPhilox, double>(c, in, table);
+    case PFMPE_STATE_F16:
+      return ref ? dispatch_m<float, kRngReference, __half>(c, in, table)
+                 : dispatch_m<float, kRngPhilox, __half>(c, in, table);
+    default:
+      return ref ? dispatch_m<float, kRngReference, float>(c, in, table)
+                 : dispatch_m<float, kRngPhilox, float>(c, in, table);
+  }
 }
 
 int dispatch_regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
-  const bool f64 = c->state_dtype == PFMPE_STATE_F64;
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
-  if (f64) return ref ? regen_m<double, kRngReference>(c, kept_iter, prior, out)
-                      : regen_m<double, kRngPhilox>(c, kept_iter, prior, out);
-  return ref ? regen_m<float, kRngReference>(c, kept_iter, prior, out)
-             : regen_m<float, kRngPhilox>(c, kept_iter, prior, out);
+  switch (c->state_dtype) {
+    case PFMPE_STATE_F64:
+      return ref ? regen_m<double, kRngReference, double>(c, kept_iter, prior, out)
+                 : regen_m<double, kRngPhilox, double>(c, kept_iter, prior, out);
+    case PFMPE_STATE_F16:
+      return ref ? regen_m<float, kRngReference, __half>(c, kept_iter, prior, out)
+                 : regen_m<float, kRngPhilox, __half>(c, kept_iter, prior, out);
+    default:
+      return ref ? regen_m<float, kRngReference, float>(c, kept_iter, prior, out)
+                 : regen_m<float, kRngPhilox, float>(c, kept_iter, prior, out);
+  }
+}
+
+// state import / export for the three storage types (anchor: fp16 state only)
+template <typename T, typename SP>
+void launch_import(pfmpe_ctx* c, int N, const double* anchor) {
+  Pose12<T> a;
+  for (int q = 0; q < 12; ++q) a.v[q] = (T)anchor[q];
+  hipLaunchKernelGGL((k_import<T, SP>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
+                     (SP*)c->d_state[c->prior_idx], N, c->ld, a);
+}
+template <typename T, typename SP>
+void launch_export(pfmpe_ctx* c, int N, const double* anchor) {
+  Pose12<T> a;
+  for (int q = 0; q < 12; ++q) a.v[q] = (T)anchor[q];
+  hipLaunchKernelGGL((k_export<T, SP>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
+                     (const SP*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld, a);
 }
 
 
@@ -90,7 +122,8 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   if (!out) return PFMPE_E_ARG;
   *out = nullptr;
   if (max_particles < 1 || max_markers < 1 || max_markers > kMaxMarkers || max_blobs < 0 ||
-      max_blobs > kMaxBlobs || (state_dtype != PFMPE_STATE_F32 && state_dtype != PFMPE_STATE_F64))
+      max_blobs > kMaxBlobs ||
+      (state_dtype != PFMPE_STATE_F32 && state_dtype != PFMPE_STATE_F64 && state_dtype != PFMPE_STATE_F16))
     return PFMPE_E_ARG;
   pfmpe_ctx* c = new pfmpe_ctx();
   c->device = hip_device;
@@ -98,7 +131,8 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   c->max_markers = max_markers;
   c->max_blobs = max_blobs;
   c->state_dtype = state_dtype;
-  c->es = state_dtype == PFMPE_STATE_F64 ? 8 : 4;
+  c->es = state_dtype == PFMPE_STATE_F64 ? 8 : (state_dtype == PFMPE_STATE_F16 ? 2 : 4);
+  c->ws = state_dtype == PFMPE_STATE_F64 ? 8 : 4;
   c->ld = ((int64_t)max_particles + 63) / 64 * 64;
   c->max_blk = (max_particles + kBlock - 1) / kBlock;
   pfmpe_default_params(&c->params);
@@ -114,7 +148,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   c->max_grp = c->max_blk;  // groups hold ~sqrt(blocks) blocks (build_args): size group buffers per block
   for (int i = 0; i < 2; ++i) {
     ok &= hipMalloc(&c->d_state[i], state_bytes) == hipSuccess;
-    ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->es) == hipSuccess;
+    ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->ws) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * sizeof(BlockPart)) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_bscan[i], (size_t)c->max_blk * sizeof(BlockScan)) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_gpart[i], (size_t)c->max_grp * sizeof(GroupPart)) == hipSuccess;
@@ -230,12 +264,14 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
   RET(set_device(c));
   RET(ensure_xfer(c));
   HIPCHK(c, hipMemcpyAsync(c->d_xfer, poses, (size_t)N * 12 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  // fp16 state: the set's anchor is its first particle (deltas of a concentrated set stay small)
+  std::memcpy(c->anchor[c->prior_idx], poses, 12 * sizeof(double));
   if (c->state_dtype == PFMPE_STATE_F64)
-    hipLaunchKernelGGL((k_import<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
-                       (double*)c->d_state[c->prior_idx], N, c->ld);
+    launch_import<double, double>(c, N, c->anchor[c->prior_idx]);
+  else if (c->state_dtype == PFMPE_STATE_F16)
+    launch_import<float, __half>(c, N, c->anchor[c->prior_idx]);
   else
-    hipLaunchKernelGGL((k_import<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream, c->d_xfer,
-                       (float*)c->d_state[c->prior_idx], N, c->ld);
+    launch_import<float, float>(c, N, c->anchor[c->prior_idx]);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
@@ -326,7 +362,10 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   c->last_accepted = o.resampled != 0;
   c->last_kept_slot = o.kept_slot;
   c->last_kept_iter = o.kept_iter;
-  if (o.resampled) c->prior_idx = 1 - c->prior_idx;  // newPoseEstimation = resampled set (PE:681, 727)
+  if (o.resampled) {  // newPoseEstimation = resampled set (PE:681, 727), anchored at this frame's current pose
+    c->prior_idx = 1 - c->prior_idx;
+    std::memcpy(c->anchor[c->prior_idx], in->current_pose, 12 * sizeof(double));
+  }
   return PFMPE_OK;
 }
 
@@ -352,11 +391,11 @@ int pfmpe_get_particles(pfmpe_ctx* c, int which, double* out) {
   if (which == 0) {
     RET(dispatch_regen(c, c->last_kept_iter, c->d_state[c->last_prior_idx], c->d_xfer));
   } else if (c->state_dtype == PFMPE_STATE_F64) {
-    hipLaunchKernelGGL((k_export<double>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
-                       (const double*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld);
+    launch_export<double, double>(c, N, c->anchor[c->prior_idx]);
+  } else if (c->state_dtype == PFMPE_STATE_F16) {
+    launch_export<float, __half>(c, N, c->anchor[c->prior_idx]);
   } else {
-    hipLaunchKernelGGL((k_export<float>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
-                       (const float*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld);
+    launch_export<float, float>(c, N, c->anchor[c->prior_idx]);
   }
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, c->d_xfer, (size_t)N * 12 * sizeof(double), hipMemcpyDeviceToHost, c->stream));

@@ -3,5 +3,5 @@
 
 namespace pfmpe_impl {
 using namespace pfmpe;
-PFMPE_DECLARE_INSTANCE(float, kRngPhilox, )
+PFMPE_DECLARE_INSTANCE(float, kRngPhilox, float, )
 }  // namespace pfmpe_impl

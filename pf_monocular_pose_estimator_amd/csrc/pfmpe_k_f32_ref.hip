@@ -3,5 +3,5 @@
 
 namespace pfmpe_impl {
 using namespace pfmpe;
-PFMPE_DECLARE_INSTANCE(float, kRngReference, )
+PFMPE_DECLARE_INSTANCE(float, kRngReference, float, )
 }  // namespace pfmpe_impl

@@ -3,5 +3,5 @@
 
 namespace pfmpe_impl {
 using namespace pfmpe;
-PFMPE_DECLARE_INSTANCE(double, kRngPhilox, )
+PFMPE_DECLARE_INSTANCE(double, kRngPhilox, double, )
 }  // namespace pfmpe_impl

@@ -3,5 +3,5 @@
 
 namespace pfmpe_impl {
 using namespace pfmpe;
-PFMPE_DECLARE_INSTANCE(double, kRngReference, )
+PFMPE_DECLARE_INSTANCE(double, kRngReference, double, )
 }  // namespace pfmpe_impl
