@@ -140,6 +140,28 @@ int pfmpe_step(pfmpe_ctx* ctx, const pfmpe_frame_in* in, pfmpe_frame_out* out);
  * overhead.  Stops at the first error; *done receives the number of frames completed. */
 int pfmpe_step_batch(pfmpe_ctx* ctx, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out, int* done);
 
+/* ---------------------------------------------------------------------- ROI prediction (§8f row 1) */
+/* predictMarkerPositionsInImage (PE:1036-1053) + LEDDetector::determineROI (led_detector.cpp:217-369),
+ * as called at PE:396-412: every marker projected through camMoveInv * prior_j * predictionMatrix for all
+ * N particles of the current prior, plus the markers at predicted_pose_; the bounding box (x_min/y_min
+ * from +inf, x_max/y_max from 0); its corners as cv::Point2f through distortPoints (plumb_bob D, in
+ * double); border, clamp to the image, integer cv::Rect (the whole image when narrower than 1 px).
+ * Call it before pfmpe_step of the same frame (the prior is the resampled set of the previous one). */
+typedef struct {
+  double cam_move_inv[12];   /* camMoveInv (PE:241-393)                                          */
+  double prediction[12];     /* predictionMatrix (PE:234)                                        */
+  double predicted_pose[12]; /* predicted_pose_ (PE:1051)                                        */
+  double D[5];               /* camera_distortion_coeffs_ k1 k2 p1 p2 k3 (led_detector.cpp:380)  */
+  int32_t image_w, image_h;  /* image.size()                                                     */
+  int32_t border;            /* roi_border_thickness_                                            */
+  int32_t pad;
+} pfmpe_roi_in;
+typedef struct {
+  int32_t x, y, width, height; /* region_of_interest_ (cv::Rect)                                 */
+  double bbox[4];              /* undistorted x_min, x_max, y_min, y_max of the projections       */
+} pfmpe_roi_out;
+int pfmpe_predict_roi(pfmpe_ctx* ctx, const pfmpe_roi_in* in, pfmpe_roi_out* out);
+
 /* getPoseParticles (PE:917, which = 0: kept propagated set of the last step) and getResampledParticles
  * (PE:923, which = 1: current prior).  N x 12 doubles. */
 int pfmpe_get_particles(pfmpe_ctx* ctx, int which, double* out);
@@ -170,8 +192,9 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* ctx, const double* blobs, const int32_t* of
 enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduce)  */
        PFMPE_K_RESAMPLE = 1,  /* k_resample (+ last-block winner / frame record)     */
        PFMPE_K_AUX = 2,       /* regeneration for pfmpe_get_particles                */
-       PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one cooperative launch  */
-       PFMPE_K_COUNT = 4 };
+       PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one launch              */
+       PFMPE_K_ROI = 4,       /* k_roi + k_roi_final (pfmpe_predict_roi)             */
+       PFMPE_K_COUNT = 5 };
 int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
 int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
 const char* pfmpe_kernel_name(int kernel);

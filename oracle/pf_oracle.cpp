@@ -773,4 +773,77 @@ int orc_optimise_pose(int M, const double* markers, const double* K, int B, cons
   return iters;
 }
 
+// ------------------------------------------------------------------ ROI prediction (§8f row 1)
+// predictMarkerPositionsInImage (PE:1036-1053) + LEDDetector::determineROI (led_detector.cpp:217-369) +
+// distortPoints (led_detector.cpp:371-414), literally: the reference's loops and cv::Point2f roundings.
+static void distort_point(const double* K, const double* D, float xin, float yin, float* xo, float* yo) {
+  const double fx_K = K[0], fy_K = K[4], cx_K = K[2], cy_K = K[5];
+  const double k1 = D[0], k2 = D[1], p1 = D[2], p2 = D[3], k3 = D[4];
+  const double px = (double)xin, py = (double)yin;  // const cv::Point2d &p = src[i] (float -> double)
+  const double x = (px - cx_K) / fx_K;
+  const double y = (py - cy_K) / fy_K;
+  const double r2 = x * x + y * y;
+  double xC = x * (1. + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2);
+  double yC = y * (1. + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2);
+  xC = xC + (2. * p1 * x * y + p2 * (r2 + 2. * x * x));
+  yC = yC + (p1 * (r2 + 2. * y * y) + 2. * p2 * x * y);
+  xC = xC * fx_K + cx_K;
+  yC = yC * fy_K + cy_K;
+  *xo = (float)xC;  // dst.push_back(cv::Point2d(...)) into a std::vector<cv::Point2f>
+  *yo = (float)yC;
+}
+
+int orc_predict_roi(int N, int M, const double* markers, const double* K, const double* D, const double* prior,
+                    const double* cam12, const double* predm12, const double* predicted12, int W, int H,
+                    int border, int* roi4, double* bbox4) {
+  const Mat4 cam = from12(cam12), predm = from12(predm12), pred = from12(predicted12);
+  std::vector<double> px, py;
+  px.reserve((size_t)(N + 1) * M);
+  py.reserve((size_t)(N + 1) * M);
+  for (int i = 0; i < M; ++i)
+    for (int j = 0; j < N; ++j) {
+      const Mat4 T = mul(mul(cam, from12(prior + 12 * (size_t)j)), predm);
+      double uv[2];
+      project2d(K, T, markers + 3 * i, uv);
+      px.push_back(uv[0]);
+      py.push_back(uv[1]);
+    }
+  for (int k = 0; k < M; ++k) {
+    double uv[2];
+    project2d(K, pred, markers + 3 * k, uv);
+    px.push_back(uv[0]);
+    py.push_back(uv[1]);
+  }
+  double x_min = INFINITY, x_max = 0, y_min = INFINITY, y_max = 0;
+  for (size_t i = 0; i < px.size(); ++i) {
+    if (px[i] < x_min) x_min = px[i];
+    if (px[i] > x_max) x_max = px[i];
+    if (py[i] < y_min) y_min = py[i];
+    if (py[i] > y_max) y_max = py[i];
+  }
+  bbox4[0] = x_min;
+  bbox4[1] = x_max;
+  bbox4[2] = y_min;
+  bbox4[3] = y_max;
+  float dx0, dy0, dx1, dy1;
+  distort_point(K, D, (float)x_min, (float)y_min, &dx0, &dy0);  // cv::Point2f(x_min, y_min)
+  distort_point(K, D, (float)x_max, (float)y_max, &dx1, &dy1);
+  const double x0 = std::max(0.0, std::min((double)W, (double)dx0 - border));
+  const double x1 = std::max(0.0, std::min((double)W, (double)dx1 + border));
+  const double y0 = std::max(0.0, std::min((double)H, (double)dy0 - border));
+  const double y1 = std::max(0.0, std::min((double)H, (double)dy1 + border));
+  if (x1 - x0 < 1 || y1 - y0 < 1) {
+    roi4[0] = 0;
+    roi4[1] = 0;
+    roi4[2] = W;
+    roi4[3] = H;
+  } else {  // cv::Rect int fields: x0 -> int, (x1 - x0) -> int (truncation)
+    roi4[0] = (int)x0;
+    roi4[1] = (int)y0;
+    roi4[2] = (int)(x1 - x0);
+    roi4[3] = (int)(y1 - y0);
+  }
+  return 0;
+}
+
 }  // extern "C"

@@ -99,6 +99,9 @@ def load() -> C.CDLL:
     lib.orc_predict_pose.argtypes = [dp, dp, C.c_double, C.c_double, C.c_double, dp, dp]
     lib.orc_optimise_pose.restype = C.c_int
     lib.orc_optimise_pose.argtypes = [C.c_int, dp, dp, C.c_int, dp, up, C.c_int, dp, dp, dp]
+    lib.orc_predict_roi.restype = C.c_int
+    lib.orc_predict_roi.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, dp, dp, C.c_int, C.c_int, C.c_int,
+                                    C.POINTER(C.c_int), dp]
     _lib = lib
     return lib
 
@@ -248,3 +251,16 @@ def optimise_pose(markers, K, blobs, pairs, pose12):
                                   pr.ctypes.data_as(C.POINTER(C.c_uint)), pr.size // 2, _p(_d(pose12).reshape(12)),
                                   _p(out), _p(cov))
     return out, cov.reshape(6, 6), it
+
+
+def predict_roi(markers, K, D, prior, cam_move_inv, prediction, predicted_pose, image_w, image_h, border):
+    """predictMarkerPositionsInImage + determineROI (PE:1036-1053, led_detector.cpp:217-414) ->
+    (roi [x, y, w, h], bbox [x_min, x_max, y_min, y_max])."""
+    m = _d(markers).reshape(-1, 3)
+    pr = _d(prior).reshape(-1, 12)
+    roi = (C.c_int * 4)()
+    bbox = np.zeros(4)
+    load().orc_predict_roi(pr.shape[0], m.shape[0], _p(m), _p(_d(K).reshape(9)), _p(_d(D).reshape(5)), _p(pr),
+                           _p(_d(cam_move_inv).reshape(12)), _p(_d(prediction).reshape(12)),
+                           _p(_d(predicted_pose).reshape(12)), image_w, image_h, border, roi, _p(bbox))
+    return list(roi), bbox

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
-K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_COUNT = 0, 1, 2, 3, 4
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_COUNT = 0, 1, 2, 3, 4, 5
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
@@ -30,6 +30,7 @@ EXPORTED_SYMBOLS = (
     "pfmpe_step", "pfmpe_step_batch", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
+    "pfmpe_predict_roi",
 )
 
 
@@ -52,6 +53,19 @@ class FrameIn(C.Structure):
         ("it_since_init", C.c_int32), ("force_iters", C.c_int32),
         ("dt", C.c_double), ("seed", C.c_uint64), ("frame_idx", C.c_uint64),
     ]
+
+
+class RoiIn(C.Structure):
+    _fields_ = [
+        ("cam_move_inv", C.c_double * 12), ("prediction", C.c_double * 12), ("predicted_pose", C.c_double * 12),
+        ("D", C.c_double * 5), ("image_w", C.c_int32), ("image_h", C.c_int32), ("border", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+class RoiOut(C.Structure):
+    _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
+                ("bbox", C.c_double * 4)]
 
 
 class FrameOut(C.Structure):
@@ -113,6 +127,7 @@ def load() -> C.CDLL:
         "pfmpe_kernel_name": (C.c_char_p, [I]),
         "pfmpe_host_ref_uniform": (D, [C.c_uint32, U64, D, D]),
         "pfmpe_host_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+        "pfmpe_predict_roi": (I, [P, C.POINTER(RoiIn), C.POINTER(RoiOut)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -235,6 +250,19 @@ class Engine:
         done = C.c_int()
         self._chk(self.lib.pfmpe_step_batch(self.ctx, arr_in, n, arr_out, C.byref(done)))
         return list(arr_out)
+
+    def predict_roi(self, prediction, predicted_pose, D, image_w, image_h, border, cam_move_inv=None) -> dict:
+        """Region of interest for the next detection (PE:396-412): {"roi": [x, y, w, h], "bbox": [...]}."""
+        ri = RoiIn()
+        cm = np.eye(4)[:3].reshape(12) if cam_move_inv is None else np.asarray(cam_move_inv, np.float64).reshape(12)
+        ri.cam_move_inv[:] = list(cm)
+        ri.prediction[:] = list(np.asarray(prediction, np.float64).reshape(12))
+        ri.predicted_pose[:] = list(np.asarray(predicted_pose, np.float64).reshape(12))
+        ri.D[:] = list(np.asarray(D, np.float64).reshape(5))
+        ri.image_w, ri.image_h, ri.border = int(image_w), int(image_h), int(border)
+        ro = RoiOut()
+        self._chk(self.lib.pfmpe_predict_roi(self.ctx, C.byref(ri), C.byref(ro)))
+        return {"roi": [ro.x, ro.y, ro.width, ro.height], "bbox": np.array(list(ro.bbox))}
 
     def get_particles(self, which: int) -> np.ndarray:
         out = np.empty((self.N, 12), dtype=np.float64)

@@ -173,27 +173,19 @@ __device__ __forceinline__ T inf_t() {
   return (T)INFINITY;
 }
 
-// thread 0 copies the kernarg arrays (compile-time indices) into LDS; callers barrier afterwards
+// The frame-constant arrays lead FrameArgsT in exactly LdsConst's layout, and FrameArgsT is every
+// kernel's first argument, so the block copies them from the kernarg segment with one vector load per
+// lane (no SGPR round trip: kept in SGPRs they spill into VGPR lanes).  Callers barrier afterwards.
 template <typename T>
 __device__ __forceinline__ void stage_consts(const FrameArgsT<T>& fa, LdsConst<T>& sc) {
-  if (threadIdx.x == 0) {
-#pragma unroll
-    for (int q = 0; q < 12; ++q) {
-      sc.cur[q] = fa.cur[q];
-      sc.pred[q] = fa.pred[q];
-      sc.predm[q] = fa.predm[q];
-      sc.cam[q] = fa.cam[q];
-    }
-#pragma unroll
-    for (int q = 0; q < kMaxMarkers * 3; ++q) sc.markers[q] = fa.markers[q];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) sc.K[q] = fa.K[q];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      sc.lo[q] = fa.lo[q];
-      sc.hi[q] = fa.hi[q];
-    }
-  }
+  static_assert(offsetof(FrameArgsT<T>, cur) == 0 && offsetof(FrameArgsT<T>, hi) == offsetof(LdsConst<T>, hi),
+                "LdsConst must mirror the head of FrameArgsT");
+  static_assert(sizeof(LdsConst<T>) % 4 == 0, "dword copy");
+  (void)fa;
+  const uint32_t* src = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t* dst = (uint32_t*)&sc;
+  constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
+  for (int i = threadIdx.x; i < kWordsC; i += kBlock) dst[i] = src[i];
 }
 
 // ----------------------------------------------------------------------------- pose algebra
@@ -1788,6 +1780,119 @@ __global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int ke
   make_particle<T, RNG, SP>(fa, sc, prior, n, kept_iter, P);
   for (int q = 0; q < 12; ++q) poses[12 * (int64_t)n + q] = (double)P[q];
 }
+// ---- ROI prediction (§8f next row 1): predictMarkerPositionsInImage (PE:1036-1053) projects every marker
+// through camMoveInv * prior_j * predictionMatrix (Eigen left-to-right products) for all N particles of
+// the current prior; LEDDetector::determineROI (led_detector.cpp:217-243) keeps x_min / y_min from +inf and
+// x_max / y_max from 0 with strict comparisons (NaN positions never win).  fp64 throughout: the same
+// arithmetic as the oracle, so the box is exact for every state type.  One partial per block, then one
+// block reduces them.
+struct RoiArgs {
+  double cam[12], predm[12], K[9], markers[kMaxMarkers * 3], anchor[12];
+  int32_t N, M;
+  int64_t ld;
+};
+template <typename T, typename SP>
+__global__ __launch_bounds__(kBlock) void k_roi(const RoiArgs ra, const SP* __restrict__ prior,
+                                               double* __restrict__ part) {
+  __shared__ double sh[4][kWaves];
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  double xmin = INFINITY, xmax = 0.0, ymin = INFINITY, ymax = 0.0;
+  if (n < ra.N) {
+    double A[12], X[12], P[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      A[q] = (double)StateIO<T, SP>::load(prior[(int64_t)q * ra.ld + n], (T)ra.anchor[q]);
+    compose(ra.cam, A, X);   // camMoveInv * newPoseEstimation[j]
+    compose(X, ra.predm, P); // ... * predictionMatrix
+    double Q[12];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        double s = ra.K[i * 3 + 0] * P[0 * 4 + j];
+        s = s + ra.K[i * 3 + 1] * P[1 * 4 + j];
+        s = s + ra.K[i * 3 + 2] * P[2 * 4 + j];
+        Q[i * 4 + j] = s;
+      }
+    for (int m = 0; m < ra.M; ++m) {
+      const double x = ra.markers[3 * m], y = ra.markers[3 * m + 1], z = ra.markers[3 * m + 2];
+      double p[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        double s = Q[i * 4 + 0] * x;
+        s = s + Q[i * 4 + 1] * y;
+        s = s + Q[i * 4 + 2] * z;
+        p[i] = s + Q[i * 4 + 3];
+      }
+      const double u = p[0] / p[2], v = p[1] / p[2];
+      if (u < xmin) xmin = u;
+      if (u > xmax) xmax = u;
+      if (v < ymin) ymin = v;
+      if (v > ymax) ymax = v;
+    }
+  }
+  xmin = wave_min(xmin);
+  xmax = wave_max(xmax);
+  ymin = wave_min(ymin);
+  ymax = wave_max(ymax);
+  const int lane = lane_id(), wv = wave_id();
+  if (lane == 0) {
+    sh[0][wv] = xmin;
+    sh[1][wv] = xmax;
+    sh[2][wv] = ymin;
+    sh[3][wv] = ymax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kWaves; ++w) {
+      xmin = sh[0][w] < xmin ? sh[0][w] : xmin;
+      xmax = sh[1][w] > xmax ? sh[1][w] : xmax;
+      ymin = sh[2][w] < ymin ? sh[2][w] : ymin;
+      ymax = sh[3][w] > ymax ? sh[3][w] : ymax;
+    }
+    double* o = part + 4 * (size_t)blockIdx.x;
+    o[0] = xmin;
+    o[1] = xmax;
+    o[2] = ymin;
+    o[3] = ymax;
+  }
+}
+template <typename T>  // (a template only for COMDAT linkage: the header is in several TUs)
+__global__ __launch_bounds__(kBlock) void k_roi_final(const T* __restrict__ part, int nblk, T* __restrict__ out) {
+  __shared__ double sh[4][kWaves];
+  double xmin = INFINITY, xmax = 0.0, ymin = INFINITY, ymax = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += kBlock) {
+    const double* o = part + 4 * (size_t)b;
+    xmin = o[0] < xmin ? o[0] : xmin;
+    xmax = o[1] > xmax ? o[1] : xmax;
+    ymin = o[2] < ymin ? o[2] : ymin;
+    ymax = o[3] > ymax ? o[3] : ymax;
+  }
+  xmin = wave_min(xmin);
+  xmax = wave_max(xmax);
+  ymin = wave_min(ymin);
+  ymax = wave_max(ymax);
+  if (lane_id() == 0) {
+    sh[0][wave_id()] = xmin;
+    sh[1][wave_id()] = xmax;
+    sh[2][wave_id()] = ymin;
+    sh[3][wave_id()] = ymax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kWaves; ++w) {
+      xmin = sh[0][w] < xmin ? sh[0][w] : xmin;
+      xmax = sh[1][w] > xmax ? sh[1][w] : xmax;
+      ymin = sh[2][w] < ymin ? sh[2][w] : ymin;
+      ymax = sh[3][w] > ymax ? sh[3][w] : ymax;
+    }
+    out[0] = xmin;
+    out[1] = xmax;
+    out[2] = ymin;
+    out[3] = ymax;
+  }
+}
+
 template <typename T>
 __global__ void k_weights_export(const T* __restrict__ w, double* __restrict__ out, int N) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;

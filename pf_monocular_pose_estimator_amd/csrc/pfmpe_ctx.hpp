@@ -58,6 +58,7 @@ struct pfmpe_ctx {
   uint32_t* d_gen = nullptr;       // k_frame iteration release word (monotonic)
   Cand* d_cand = nullptr;          // per-block winner candidates
   double* d_mlpose = nullptr;      // most likely pose (12)
+  double* d_roi = nullptr;         // ROI box [4] + per-block partials
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
   bool fused = true;               // PFMPE_OPT_FUSED

@@ -81,7 +81,7 @@ void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* 
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
-                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_roi, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -380,6 +380,109 @@ int pfmpe_step_batch(pfmpe_ctx* c, const pfmpe_frame_in* in, int n, pfmpe_frame_
   return PFMPE_OK;
 }
 
+namespace {
+// project2d (PE:1017-1034) in double on the host: (K34 * T) * [X;1], then / z
+void host_project(const double* K, const double* T12, const double* X, double* uv) {
+  double Q[12];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) {
+      double s = K[i * 3 + 0] * T12[0 * 4 + j];
+      s = s + K[i * 3 + 1] * T12[1 * 4 + j];
+      s = s + K[i * 3 + 2] * T12[2 * 4 + j];
+      Q[i * 4 + j] = s;
+    }
+  double p[3];
+  for (int i = 0; i < 3; ++i) {
+    double s = Q[i * 4 + 0] * X[0];
+    s = s + Q[i * 4 + 1] * X[1];
+    s = s + Q[i * 4 + 2] * X[2];
+    p[i] = s + Q[i * 4 + 3];
+  }
+  uv[0] = p[0] / p[2];
+  uv[1] = p[1] / p[2];
+}
+// LEDDetector::distortPoints (led_detector.cpp:371-414) on cv::Point2f inputs, result back to float
+void host_distort(const double* K, const double* D, float xin, float yin, float* xo, float* yo) {
+  const double fx = K[0], fy = K[4], cx = K[2], cy = K[5];
+  const double k1 = D[0], k2 = D[1], p1 = D[2], p2 = D[3], k3 = D[4];
+  const double x = ((double)xin - cx) / fx;
+  const double y = ((double)yin - cy) / fy;
+  const double r2 = x * x + y * y;
+  double xc = x * (1. + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2);
+  double yc = y * (1. + k1 * r2 + k2 * r2 * r2 + k3 * r2 * r2 * r2);
+  xc = xc + (2. * p1 * x * y + p2 * (r2 + 2. * x * x));
+  yc = yc + (p1 * (r2 + 2. * y * y) + 2. * p2 * x * y);
+  *xo = (float)(xc * fx + cx);
+  *yo = (float)(yc * fy + cy);
+}
+}  // namespace
+
+int pfmpe_predict_roi(pfmpe_ctx* c, const pfmpe_roi_in* in, pfmpe_roi_out* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!in || !out) return fail(c, PFMPE_E_ARG, "predict_roi: null in/out");
+  if (!c->has_model || !c->has_prior) return fail(c, PFMPE_E_STATE, "predict_roi: set_model and set_prior first");
+  if (in->image_w < 1 || in->image_h < 1) return fail(c, PFMPE_E_ARG, "predict_roi: bad image size");
+  RET(set_device(c));
+  const int N = c->N;
+  const int nblk = (N + kBlock - 1) / kBlock;
+  if (!c->d_roi) HIPCHK(c, hipMalloc((void**)&c->d_roi, ((size_t)c->max_blk + 1) * 4 * sizeof(double)));
+  RoiArgs ra{};
+  std::memcpy(ra.cam, in->cam_move_inv, sizeof(ra.cam));
+  std::memcpy(ra.predm, in->prediction, sizeof(ra.predm));
+  std::memcpy(ra.K, c->K, sizeof(ra.K));
+  std::memcpy(ra.markers, c->markers, sizeof(ra.markers));
+  std::memcpy(ra.anchor, c->anchor[c->prior_idx], sizeof(ra.anchor));
+  ra.N = N;
+  ra.M = c->M;
+  ra.ld = c->ld;
+  double* part = c->d_roi + 4;
+  RET(launch(c, PFMPE_K_ROI, [&] {
+    const void* st = c->d_state[c->prior_idx];
+    if (c->state_dtype == PFMPE_STATE_F64)
+      hipLaunchKernelGGL((k_roi<double, double>), dim3(nblk), dim3(kBlock), 0, c->stream, ra, (const double*)st, part);
+    else if (c->state_dtype == PFMPE_STATE_F16)
+      hipLaunchKernelGGL((k_roi<float, __half>), dim3(nblk), dim3(kBlock), 0, c->stream, ra, (const __half*)st, part);
+    else
+      hipLaunchKernelGGL((k_roi<float, float>), dim3(nblk), dim3(kBlock), 0, c->stream, ra, (const float*)st, part);
+    hipLaunchKernelGGL((k_roi_final<double>), dim3(1), dim3(kBlock), 0, c->stream, part, nblk, c->d_roi);
+  }));
+  double bb[4];
+  HIPCHK(c, hipMemcpyAsync(bb, c->d_roi, sizeof(bb), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->ev_used = 0;
+  // + the markers at predicted_pose_ (PE:1049-1052)
+  for (int m = 0; m < c->M; ++m) {
+    double uv[2];
+    host_project(c->K, in->predicted_pose, c->markers + 3 * m, uv);
+    if (uv[0] < bb[0]) bb[0] = uv[0];
+    if (uv[0] > bb[1]) bb[1] = uv[0];
+    if (uv[1] < bb[2]) bb[2] = uv[1];
+    if (uv[1] > bb[3]) bb[3] = uv[1];
+  }
+  std::memcpy(out->bbox, bb, sizeof(bb));
+  // determineROI (led_detector.cpp:317-368): corners as cv::Point2f, distorted, border, clamp, cv::Rect
+  float x0f, y0f, x1f, y1f;
+  host_distort(c->K, in->D, (float)bb[0], (float)bb[2], &x0f, &y0f);
+  host_distort(c->K, in->D, (float)bb[1], (float)bb[3], &x1f, &y1f);
+  const double W = in->image_w, H = in->image_h, b = in->border;
+  const double x0 = std::max(0.0, std::min(W, (double)x0f - b));
+  const double x1 = std::max(0.0, std::min(W, (double)x1f + b));
+  const double y0 = std::max(0.0, std::min(H, (double)y0f - b));
+  const double y1 = std::max(0.0, std::min(H, (double)y1f + b));
+  if (x1 - x0 < 1 || y1 - y0 < 1) {
+    out->x = 0;
+    out->y = 0;
+    out->width = in->image_w;
+    out->height = in->image_h;
+  } else {
+    out->x = (int32_t)x0;
+    out->y = (int32_t)y0;
+    out->width = (int32_t)(x1 - x0);
+    out->height = (int32_t)(y1 - y0);
+  }
+  return PFMPE_OK;
+}
+
 int pfmpe_get_particles(pfmpe_ctx* c, int which, double* out) {
   if (!c) return PFMPE_E_ARG;
   if (!out || (which != 0 && which != 1)) return fail(c, PFMPE_E_ARG, "get_particles: bad arguments");
@@ -476,7 +579,7 @@ int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
 }
 
 const char* pfmpe_kernel_name(int kernel) {
-  static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux", "k_frame"};
+  static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux", "k_frame", "k_roi"};
   return (kernel >= 0 && kernel < PFMPE_K_COUNT) ? names[kernel] : "?";
 }
 

@@ -18,7 +18,7 @@ from oracle import pforacle as orc
 pytestmark = pytest.mark.gpu
 
 RNG = {"ref": pf.RNG_REFERENCE, "philox": pf.RNG_PHILOX}
-STATE = {"f64": pf.STATE_F64, "f32": pf.STATE_F32}
+STATE = {"f64": pf.STATE_F64, "f32": pf.STATE_F32, "f16": pf.STATE_F16}
 
 
 def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None, fused=True):
@@ -477,3 +477,38 @@ def test_fp16_state_tracks_fp32():
         assert rotation_angle(syn.to44(pa)[:3, :3], syn.to44(pb)[:3, :3]) < 1e-3
     assert same >= 25, same
     assert compared >= 20, its
+
+
+@pytest.mark.parametrize("state", ["f64", "f32", "f16"])
+def test_predict_roi_matches_oracle(state):
+    """ROI prediction (§8f next row 1, PE:396-412): the GPU box over N x M projections of
+    camMoveInv * prior_j * predictionMatrix plus the predicted pose, then the reference's corner
+    distortion / clamp / cv::Rect, against the oracle on the engine's own prior: bit-exact box, equal ROI."""
+    N = 30_000
+    cfg = syn.StreamConfig("t", M=5, B=50, N=N)
+    st = syn.make_stream(cfg, 3)
+    eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX)
+    eng.set_prior(st.prior())
+    cam = np.eye(4)
+    cam[:3, 3] = [0.01, -0.004, 0.002]
+    for fr in st.frames:
+        prior = eng.get_particles(1)
+        for cm, border in ((None, 20), (cam[:3].reshape(12), 5)):
+            got = eng.predict_roi(fr.prediction, fr.predicted_pose, syn.D_README, syn.IMAGE_W, syn.IMAGE_H, border,
+                                  cam_move_inv=cm)
+            roi, bbox = orc.predict_roi(st.markers, st.K, syn.D_README, prior,
+                                        np.eye(4)[:3].reshape(12) if cm is None else cm, fr.prediction,
+                                        fr.predicted_pose, syn.IMAGE_W, syn.IMAGE_H, border)
+            assert np.array_equal(got["bbox"], bbox), (got["bbox"], bbox)
+            assert got["roi"] == roi
+        eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt,
+                                seed=7 + fr.index, frame_idx=fr.index))
+    # prediction far outside the image: the whole image
+    far = np.eye(4)[:3].reshape(12).copy()
+    far[11] = -5.0  # behind the camera: mirrored projections
+    got = eng.predict_roi(np.eye(4)[:3].reshape(12), far, syn.D_README, syn.IMAGE_W, syn.IMAGE_H, 10,
+                          cam_move_inv=far)
+    roi, _ = orc.predict_roi(st.markers, st.K, syn.D_README, eng.get_particles(1), far,
+                             np.eye(4)[:3].reshape(12), far, syn.IMAGE_W, syn.IMAGE_H, 10)
+    assert got["roi"] == roi
+    eng.close()
