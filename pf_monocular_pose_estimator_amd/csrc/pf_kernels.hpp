@@ -352,6 +352,10 @@ __host__ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
   if (f >= (T)(kBuckets - 1)) return kBuckets - 1;
   return (int)f;
 }
+template <typename T>
+struct alignas(2 * sizeof(T)) BlobXY {
+  T x, y;
+};
 
 // calculateEstimationProbability (PE:2385-2445) in its closed form.  Step 1: per marker the first-minimum
 // blob over all blobs (column minimum of the B x M distance matrix; ties -> lowest blob index).
@@ -359,38 +363,45 @@ __host__ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
 // visitor finds them — with the same gate (tol_PF), score ((tol-d)/tol)^2 with tol NOT tol_PF,
 // self-occlusion (3*s) and downgrade (2) penalties, capped at min(B, M) pairs.
 //
-// Exact pruning (DESIGN.md "Exact blob pruning"): only blobs inside the x-window |bx-u| <= tolq
-// (tolq >= tol_PF plus rounding slack) are visited.  Every blob within tol_PF lies in the window, and a
-// marker whose true minimum lies outside it fails the gate anyway, so accepted pairs, penalties and the
-// weight are unchanged; rejected markers only change their (unused) distance value.
+// Exact pruning (DESIGN.md "Exact blob pruning"): only blobs in the x-buckets overlapping the window
+// |bx-u| <= tolq (tolq >= tol_PF plus rounding slack) are visited.  Every blob within tol_PF lies in the
+// window, and a marker whose true minimum lies outside it fails the gate anyway, so accepted pairs,
+// penalties and the weight are unchanged; rejected markers only change their (unused) distance value.
+// (A 2D cell grid was measured slower: the extra cell arithmetic and nested row loop cost more than the
+// candidates it prunes.)  Candidates are read as packed (x, y); the original index is read only on an
+// exact distance tie (lowest index wins).
+template <typename T>
+struct LdsBlobs;
+
 template <typename T, int MAXM, bool PRUNE>
-__device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* u, const T* v, const T* bx,
-                                              const T* by, const int32_t* orig, const int32_t* bstart,
-                                              T xmin, T inv_bw, T* m, int* r) {
+__device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* u, const T* v,
+                                              const LdsBlobs<T>& tb, T* m, int* r) {
   const int B = fa.B, M = fa.M;
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     T best = inf_t<T>();
-    int arg = 0x7fffffff;
+    int bc = -1;  // table position of the current minimum
     if (j < M) {
       int c0 = 0, c1 = B;
       if (PRUNE) {
-        c0 = bstart[bucket_of(u[j] - fa.tolq, xmin, inv_bw)];
-        c1 = bstart[bucket_of(u[j] + fa.tolq, xmin, inv_bw) + 1];
+        c0 = tb.bstart[bucket_of(u[j] - fa.tolq, tb.xmin, tb.inv_bw)];
+        c1 = tb.bstart[bucket_of(u[j] + fa.tolq, tb.xmin, tb.inv_bw) + 1];
       }
       for (int c = c0; c < c1; ++c) {
-        const T dx = bx[c] - u[j];
-        const T dy = by[c] - v[j];
+        const BlobXY<T> p = tb.bxy[c];
+        const T dx = p.x - u[j];
+        const T dy = p.y - v[j];
         const T d = fmadd(dx, dx, dy * dy);
-        const int o = orig[c];
-        if (d < best || (d == best && o < arg)) {
+        if (d < best) {
           best = d;
-          arg = o;
+          bc = c;
+        } else if (d == best && bc >= 0 && tb.orig[c] < tb.orig[bc]) {
+          bc = c;
         }
       }
     }
     m[j] = best;
-    r[j] = (arg == 0x7fffffff) ? 0 : arg;
+    r[j] = bc >= 0 ? tb.orig[bc] : 0;
   }
 }
 
@@ -759,24 +770,21 @@ __device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
 // ============================================================================== kernels
 // ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into kBuckets x-buckets,
 // built once per frame on the host (build_blob_table_host, O(B)) and copied whole into each block's
-// LDS by k_propagate_weigh.  Layout, every part 16-byte aligned:
-//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[kBuckets+1] | T bx[B] | T by[B] | int32 orig[B]
-// Within a bucket blobs keep increasing original index; candidate minima use the explicit
-// (distance, original index) order anyway, so no result depends on the bucket order.
+// LDS by the weighing pass.  Layout, every part 16-byte aligned:
+//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[kBuckets+1] | BlobXY<T> xy[B] | int32 orig[B]
+// Within a bucket blobs keep increasing original index.
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 template <typename T>
 struct BlobTable {
   static constexpr size_t off_bstart() { return align16(4 * sizeof(T)); }
-  static constexpr size_t off_bx() { return off_bstart() + align16((kBuckets + 1) * 4); }
-  static constexpr size_t off_by(int B) { return off_bx() + align16((size_t)B * sizeof(T)); }
-  static constexpr size_t off_orig(int B) { return off_by(B) + align16((size_t)B * sizeof(T)); }
+  static constexpr size_t off_xy() { return off_bstart() + align16((kBuckets + 1) * 4); }
+  static constexpr size_t off_orig(int B) { return off_xy() + align16((size_t)B * sizeof(BlobXY<T>)); }
   static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
 };
 
 template <typename T>
 struct LdsBlobs {
-  const T* bx;
-  const T* by;
+  const BlobXY<T>* bxy;
   const int32_t* orig;
   const int32_t* bstart;  // kBuckets + 1
   T xmin, inv_bw, b0x, b0y;
@@ -791,8 +799,7 @@ __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* 
   t.b0x = hdr[2];
   t.b0y = hdr[3];
   t.bstart = (const int32_t*)(base + BlobTable<T>::off_bstart());
-  t.bx = (const T*)(base + BlobTable<T>::off_bx());
-  t.by = (const T*)(base + BlobTable<T>::off_by(B));
+  t.bxy = (const BlobXY<T>*)(base + BlobTable<T>::off_xy());
   t.orig = (const int32_t*)(base + BlobTable<T>::off_orig(B));
   return t;
 }
@@ -820,8 +827,7 @@ inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst
   hdr[2] = B > 0 ? (T)blobs[0] : (T)0;
   hdr[3] = B > 0 ? (T)blobs[1] : (T)0;
   int32_t* bstart = (int32_t*)(dst + BlobTable<T>::off_bstart());
-  T* bx = (T*)(dst + BlobTable<T>::off_bx());
-  T* by = (T*)(dst + BlobTable<T>::off_by(B));
+  BlobXY<T>* xy = (BlobXY<T>*)(dst + BlobTable<T>::off_xy());
   int32_t* orig = (int32_t*)(dst + BlobTable<T>::off_orig(B));
   int32_t cnt[kBuckets + 1] = {0};
   for (int i = 0; i < B; ++i) ++cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw) + 1];
@@ -829,8 +835,8 @@ inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst
   for (int b = 0; b <= kBuckets; ++b) bstart[b] = cnt[b];
   for (int i = 0; i < B; ++i) {
     const int pos = cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw)]++;
-    bx[pos] = (T)blobs[2 * i];
-    by[pos] = (T)blobs[2 * i + 1];
+    xy[pos].x = (T)blobs[2 * i];
+    xy[pos].y = (T)blobs[2 * i + 1];
     orig[pos] = i;
   }
 }
@@ -1106,7 +1112,7 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
   if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
     T m[MAXM];
     int r[MAXM];
-    column_minima<T, MAXM, PRUNE>(fa, u, v, tb.bx, tb.by, tb.orig, tb.bstart, tb.xmin, tb.inv_bw, m, r);
+    column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
     w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
   }
   return w;
@@ -1261,7 +1267,8 @@ __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsCon
     arg[j] = 0x7fffffff;
   }
   for (int i = lane; i < B; i += 64) {
-    const T bx = tb.bx[i], by = tb.by[i];
+    const BlobXY<T> p = tb.bxy[i];
+    const T bx = p.x, by = p.y;
     const int o = tb.orig[i];
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
