@@ -48,7 +48,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kGroup = 64;
 constexpr int kMaxMarkers = 16;
 constexpr int kMaxBlobs = 1024;
-constexpr int kBuckets = 128;          // x-buckets of the blob table
+constexpr int kMaxBuckets = 512;       // x-buckets of the blob table (see bucket_count)
 constexpr int kMaxIter = 4096;         // PF iterations per frame (reference: 80); < 2^16 for k_frame's release tags
 constexpr int kPlanes = 12;            // r00 r01 r02 t0 r10 r11 r12 t1 r20 r21 r22 t2
 
@@ -344,12 +344,19 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
   }
 }
 
+// x-buckets per frame: 2 per blob rounded up to a power of two, in [128, kMaxBuckets] — narrow enough
+// that the +-tolq window stays close to its own width when B is large (C3: 200 blobs, 1.5 px buckets)
+__host__ __device__ __forceinline__ constexpr int bucket_count(int B) {
+  int nb = 128;
+  while (nb < kMaxBuckets && nb < 2 * B) nb *= 2;
+  return nb;
+}
 // x -> bucket index (monotone in x; identical formula for table build and queries)
 template <typename T>
-__host__ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw) {
+__host__ __device__ __forceinline__ int bucket_of(T x, T xmin, T inv_bw, int nb) {
   const T f = (x - xmin) * inv_bw;
   if (!(f >= (T)0)) return 0;
-  if (f >= (T)(kBuckets - 1)) return kBuckets - 1;
+  if (f >= (T)(nb - 1)) return nb - 1;
   return (int)f;
 }
 template <typename T>
@@ -374,9 +381,10 @@ template <typename T>
 struct LdsBlobs;
 
 template <typename T, int MAXM, bool PRUNE>
-__device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* u, const T* v,
-                                              const LdsBlobs<T>& tb, T* m, int* r) {
+__device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u, const T* v,
+                                             const LdsBlobs<T>& tb, T* m, int* r) {
   const int B = fa.B, M = fa.M;
+  int visited = 0;
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     T best = inf_t<T>();
@@ -384,11 +392,11 @@ __device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* 
     if (j < M) {
       int c0 = 0, c1 = B;
       if (PRUNE) {
-        c0 = tb.bstart[bucket_of(u[j] - fa.tolq, tb.xmin, tb.inv_bw)];
-        c1 = tb.bstart[bucket_of(u[j] + fa.tolq, tb.xmin, tb.inv_bw) + 1];
+        c0 = tb.bstart[bucket_of(u[j] - fa.tolq, tb.xmin, tb.inv_bw, tb.nb)];
+        c1 = tb.bstart[bucket_of(u[j] + fa.tolq, tb.xmin, tb.inv_bw, tb.nb) + 1];
       }
-      for (int c = c0; c < c1; ++c) {
-        const BlobXY<T> p = tb.bxy[c];
+      visited += c1 - c0;
+      auto visit = [&](int c, BlobXY<T> p) {
         const T dx = p.x - u[j];
         const T dy = p.y - v[j];
         const T d = fmadd(dx, dx, dy * dy);
@@ -398,11 +406,19 @@ __device__ __forceinline__ void column_minima(const FrameArgsT<T>& fa, const T* 
         } else if (d == best && bc >= 0 && tb.orig[c] < tb.orig[bc]) {
           bc = c;
         }
+      };
+      int c = c0;
+      for (; c + 1 < c1; c += 2) {  // two candidates' LDS reads in flight per step
+        const BlobXY<T> pa = tb.bxy[c], pb = tb.bxy[c + 1];
+        visit(c, pa);
+        visit(c + 1, pb);
       }
+      if (c < c1) visit(c, tb.bxy[c]);
     }
     m[j] = best;
     r[j] = bc >= 0 ? tb.orig[bc] : 0;
   }
+  return visited;
 }
 
 // Eigen's visitor starts from coeff(0,0): a NaN distance there poisons the first minCoeff -> break at k=0
@@ -768,17 +784,18 @@ __device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
 }
 
 // ============================================================================== kernels
-// ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into kBuckets x-buckets,
+// ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into bucket_count(B) x-buckets,
 // built once per frame on the host (build_blob_table_host, O(B)) and copied whole into each block's
 // LDS by the weighing pass.  Layout, every part 16-byte aligned:
-//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[kBuckets+1] | BlobXY<T> xy[B] | int32 orig[B]
+//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[nb+1] | BlobXY<T> xy[B] | int32 orig[B]
+// with nb = bucket_count(B).
 // Within a bucket blobs keep increasing original index.
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 template <typename T>
 struct BlobTable {
   static constexpr size_t off_bstart() { return align16(4 * sizeof(T)); }
-  static constexpr size_t off_xy() { return off_bstart() + align16((kBuckets + 1) * 4); }
-  static constexpr size_t off_orig(int B) { return off_xy() + align16((size_t)B * sizeof(BlobXY<T>)); }
+  static constexpr size_t off_xy(int B) { return off_bstart() + align16((size_t)(bucket_count(B) + 1) * 4); }
+  static constexpr size_t off_orig(int B) { return off_xy(B) + align16((size_t)B * sizeof(BlobXY<T>)); }
   static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
 };
 
@@ -786,8 +803,9 @@ template <typename T>
 struct LdsBlobs {
   const BlobXY<T>* bxy;
   const int32_t* orig;
-  const int32_t* bstart;  // kBuckets + 1
+  const int32_t* bstart;  // nb + 1
   T xmin, inv_bw, b0x, b0y;
+  int nb;
 };
 
 template <typename T>
@@ -798,8 +816,9 @@ __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* 
   t.inv_bw = hdr[1];
   t.b0x = hdr[2];
   t.b0y = hdr[3];
+  t.nb = bucket_count(B);
   t.bstart = (const int32_t*)(base + BlobTable<T>::off_bstart());
-  t.bxy = (const BlobXY<T>*)(base + BlobTable<T>::off_xy());
+  t.bxy = (const BlobXY<T>*)(base + BlobTable<T>::off_xy(B));
   t.orig = (const int32_t*)(base + BlobTable<T>::off_orig(B));
   return t;
 }
@@ -820,21 +839,22 @@ inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst
   }
   T span = xmax - xmin;
   if (!(span > (T)0)) span = (T)1;
-  const T inv_bw = (T)kBuckets / span;
+  const int nb = bucket_count(B);
+  const T inv_bw = (T)nb / span;
   T* hdr = (T*)dst;
   hdr[0] = xmin;
   hdr[1] = inv_bw;
   hdr[2] = B > 0 ? (T)blobs[0] : (T)0;
   hdr[3] = B > 0 ? (T)blobs[1] : (T)0;
   int32_t* bstart = (int32_t*)(dst + BlobTable<T>::off_bstart());
-  BlobXY<T>* xy = (BlobXY<T>*)(dst + BlobTable<T>::off_xy());
+  BlobXY<T>* xy = (BlobXY<T>*)(dst + BlobTable<T>::off_xy(B));
   int32_t* orig = (int32_t*)(dst + BlobTable<T>::off_orig(B));
-  int32_t cnt[kBuckets + 1] = {0};
-  for (int i = 0; i < B; ++i) ++cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw) + 1];
-  for (int b = 0; b < kBuckets; ++b) cnt[b + 1] += cnt[b];
-  for (int b = 0; b <= kBuckets; ++b) bstart[b] = cnt[b];
+  int32_t cnt[kMaxBuckets + 1] = {0};
+  for (int i = 0; i < B; ++i) ++cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw, nb) + 1];
+  for (int b = 0; b < nb; ++b) cnt[b + 1] += cnt[b];
+  for (int b = 0; b <= nb; ++b) bstart[b] = cnt[b];
   for (int i = 0; i < B; ++i) {
-    const int pos = cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw)]++;
+    const int pos = cnt[bucket_of((T)blobs[2 * i], xmin, inv_bw, nb)]++;
     xy[pos].x = (T)blobs[2 * i];
     xy[pos].y = (T)blobs[2 * i + 1];
     orig[pos] = i;
@@ -1104,7 +1124,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
 // ---- one particle through the motion model, projection and likelihood (PE:543-604, PE:2385)
 template <typename T, int RNG, int MAXM, bool PRUNE>
 __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
-                                            const T* A, int n, int iter, T* P) {
+                                            const T* A, int n, int iter, T* P, int* nvisit = nullptr) {
   T u[MAXM], v[MAXM];
   propagate<T, RNG>(fa, sc, A, n, iter, P);
   project_markers<T, MAXM>(fa, sc, P, u, v);
@@ -1112,7 +1132,8 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
   if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
     T m[MAXM];
     int r[MAXM];
-    column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
+    const int visited = column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
+    if (nvisit) *nvisit = visited;
     w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
   }
   return w;
@@ -1229,8 +1250,11 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   T w = (T)0;
   if (valid) {
     T P[12];
-    w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
+    int nv = 0;
+    w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P, &nv);
     (slot ? w1 : w0)[n] = w;
+    if (stamps && (fa.diag & 8))  // diagnostic: pruned candidates visited (sum, max)
+      atomicAdd((unsigned long long*)(stamps + 30), (unsigned long long)nv), atomicMax((unsigned long long*)(stamps + 31), (unsigned long long)nv);
   }
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
   publish_iteration<T, RNG>(fa, w, valid, n, slot, iter, sh, part0, part1, bscan0, bscan1, gpart0, gpart1, gscan,

@@ -7,10 +7,11 @@ lib = pf.load()
 lib.pfmpe_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
 fused = int(os.environ.get('PFMPE_FUSED', '1'))
 for N in [int(x) for x in sys.argv[1:]] or [100000]:
-    cfg = syn.StreamConfig("C2", M=5, B=50, N=N)
+    base = syn.CONFIGS[os.environ.get("PFMPE_CFG", "C2")]
+    cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=N, heavy=base.heavy)
     st = syn.make_stream(cfg, 30)
     eng = pf.Engine(0, N); eng.set_model(st.markers, st.K); eng.set_params(pf.default_params()); eng.set_prior(st.prior())
-    eng.set_option(99, 4)
+    eng.set_option(99, 4 | 8)
     eng.set_option(pf.OPT_FUSED, fused)
     rows = []
     for fr in st.frames:
@@ -28,6 +29,8 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
              11: "K2 counts (last)", 12: "K2 scatter (last)", 13: "fin Pm", 14: "fin P", 15: "fin minima",
              16: "fin score", 17: "fin record", 18: "fin published", 20: "K2 block argmax (last)",
              21: "K2 rows staged (last)", 1: "K1 block partial (last)", 5: "K2 block partial (last)"}
+    raw = np.array(list(s), dtype=np.float64)
+    print(f"    candidates visited per particle: mean {raw[30] / N:.1f}  max {raw[31]:.0f}  (last frame, {cfg.M} markers)")
     for i in sorted(names, key=lambda i: r[i]):
         print(f"    {names[i]:24s} {r[i]:8.2f}")
     eng.close()
