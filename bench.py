@@ -62,6 +62,7 @@ def algorithmic_bytes(S: int, N: int) -> dict:
         "k_propagate_weigh": N * (S + 4),      # read prior state, write weight
         "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
         "k_frame": N * (S + 4 + S),             # one launch: read prior, write weight, write new prior
+        "k_resample_final": 8 * -(-N // 256),   # read the block count partials
         "aux": 0,
     }
 

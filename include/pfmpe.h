@@ -190,11 +190,12 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* ctx, const double* blobs, const int32_t* of
 /* Per-kernel statistics collected while PFMPE_OPT_TIMING is on: launches and summed device time (ms)
  * measured with HIP events on the ctx stream. */
 enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduce)  */
-       PFMPE_K_RESAMPLE = 1,  /* k_resample (+ last-block winner / frame record)     */
+       PFMPE_K_RESAMPLE = 1,  /* k_resample: resampling + block count partials       */
        PFMPE_K_AUX = 2,       /* regeneration for pfmpe_get_particles                */
        PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one launch              */
        PFMPE_K_ROI = 4,       /* k_roi + k_roi_final (pfmpe_predict_roi)             */
-       PFMPE_K_COUNT = 5 };
+       PFMPE_K_FINAL = 5,     /* k_resample_final: winner + frame record (one block) */
+       PFMPE_K_COUNT = 6 };
 int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
 int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
 const char* pfmpe_kernel_name(int kernel);

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
-K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_COUNT = 0, 1, 2, 3, 4, 5
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5, 6
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (

@@ -344,6 +344,33 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
   }
 }
 
+// project_markers' arithmetic for ONE marker j (wave-uniform index): the same operation order, so the
+// same bits
+template <typename T>
+__device__ __forceinline__ void project_one(const LdsConst<T>& sc, const T* P, int j, T& u, T& v) {
+  T Q[12];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      T s = sc.K[i * 3 + 0] * P[0 * 4 + c];
+      s = fmadd(sc.K[i * 3 + 1], P[1 * 4 + c], s);
+      s = fmadd(sc.K[i * 3 + 2], P[2 * 4 + c], s);
+      Q[i * 4 + c] = s;
+    }
+  }
+  const T X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
+  T p[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    T s = Q[i * 4 + 0] * X;
+    s = fmadd(Q[i * 4 + 1], Y, s);
+    s = fmadd(Q[i * 4 + 2], Z, s);
+    p[i] = s + Q[i * 4 + 3];
+  }
+  persp(p[0], p[1], p[2], &u, &v);
+}
+
 // x-buckets per frame: 2 per blob rounded up to a power of two, in [128, kMaxBuckets] — narrow enough
 // that the +-tolq window stays close to its own width when B is large (C3: 200 blobs, 1.5 px buckets)
 __host__ __device__ __forceinline__ constexpr int bucket_count(int B) {
@@ -1275,6 +1302,50 @@ struct alignas(16) Cand {
 // correspondences (PE:2385-2445 with pairs) of ONE pose P (uniform across the wave): blobs spread over
 // the lanes, (distance, original index) order as column_minima, then the sorting-network score.
 // Pairs go to corr (LDS), written by lane 0.
+// The pairs score_minima<PAIRS> lists (PE:2385-2445) from the per-marker minima m / blob indices r (uniform
+// across the wave); u0, v0: marker 0's projection (the NaN-at-origin rule).  One whole wave; corr: the
+// 2*kMaxMarkers LDS words of the (LED, blob) pairs, cleared first.  Returns the pair count.
+template <typename T, int MAXM>
+__device__ __forceinline__ int pairs_from_minima(const FrameArgsT<T>& fa, const LdsBlobs<T>& tb, const T* m,
+                                                 const int* r, T u0, T v0, uint32_t* corr) {
+  const int lane = lane_id();
+  const int B = fa.B;
+  if (lane < 2 * kMaxMarkers) corr[lane] = 0u;
+  wave_lds_sync();  // the pairs are written over the cleared words
+  // The pairs score_minima<PAIRS> lists (PE:2385-2445), lane-parallel: the keys (m_j, j) in ascending
+  // order, cut at the first key whose distance fails the tol_PF gate and at min(B, M).  Lane j < MAXM
+  // holds key j (+inf past M, as in score_minima) and computes its rank; keys are distinct, so the ranks
+  // are exactly the sorted positions.
+  int np = 0;
+  if (B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u0, v0)) {
+    const int M = fa.M;
+    const int L = B < M ? B : M;
+    T mj = inf_t<T>();
+    int rj = 0;
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      mj = (lane == j && j < M) ? m[j] : mj;
+      rj = lane == j ? r[j] : rj;
+    }
+    int rank = 0;
+#pragma unroll
+    for (int i = 0; i < MAXM; ++i) {
+      const T mi = i < M ? m[i] : inf_t<T>();
+      rank += (mi < mj || (mi == mj && i < lane)) ? 1 : 0;
+    }
+    const bool key = lane < MAXM;
+    const bool fail = !(sqrt_t(mj) <= fa.tol_pf);
+    const int fr = (key && fail) ? rank : MAXM;
+    const int F = -lane_value(wave_scan(-fr, -MAXM, OpMaxI()), 63);  // first failing rank
+    np = F < L ? F : L;
+    if (key && rank < np) {
+      corr[2 * rank] = (uint32_t)lane + 1u;
+      corr[2 * rank + 1] = (uint32_t)rj + 1u;
+    }
+  }
+  wave_lds_sync();
+  return np;
+}
 template <typename T, int MAXM>
 __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
                                            const T* P, uint32_t* corr, int* np_out) {
@@ -1305,19 +1376,14 @@ __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsCon
       }
     }
   }
+  // all MAXM reductions unconditionally (markers past M reduce +inf: harmless), so the DPP chains interleave
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
-    if (j < fa.M) wave_argmin(best[j], arg[j]);  // uniform branch
+    wave_argmin(best[j], arg[j]);
     m[j] = best[j];
     r[j] = arg[j] == 0x7fffffff ? 0 : arg[j];
   }
-  if (lane < 2 * kMaxMarkers) corr[lane] = 0u;
-  wave_lds_sync();  // lane 0 writes the pairs over the cleared words
-  int np = 0;
-  if (lane == 0 && B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0]))
-    score_minima<T, MAXM, true>(fa, m, r, corr, &np);
-  *np_out = lane_value(np, 0);
-  wave_lds_sync();
+  *np_out = pairs_from_minima<T, MAXM>(fa, tb, m, r, u[0], v[0], corr);
 }
 
 // ---- frame record (one wave) into pinned host memory: the scalars from the control record, the
@@ -1329,17 +1395,18 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
                                                Ctrl* __restrict__ ctrl, const SP* __restrict__ prior, int winner,
                                                const Cand* __restrict__ cand, const double* __restrict__ mlpose,
                                                OutDev& rec, OutDev* __restrict__ out, int32_t tag,
-                                               uint64_t* __restrict__ stamps) {
+                                               uint64_t* __restrict__ stamps, bool have_pl = false,
+                                               uint32_t pl_reg = 0u, double ml_reg = 0.0) {
   const int lane = lane_id();
   if (c.accepted) {
-    // the winner's candidate granules (one round trip; re-polled, bounded, while a tag is stale) and the
-    // most likely pose
+    // the winner's candidate granules (one round trip; re-polled, bounded, while a tag is stale; or
+    // handed over in registers, have_pl) and the most likely pose
     const Cand* wc = cand + winner / kBlock;
-    double ml = 0.0;
-    if (lane < 12) ml = ld_wt_d(mlpose + lane);
-    uint64_t gv = 0;
+    double ml = ml_reg;
+    if (lane < 12 && !have_pl) ml = ld_wt_d(mlpose + lane);
+    uint64_t gv = pl_reg;
     const uint64_t t0 = rt_now();
-    for (;;) {
+    for (; !have_pl;) {
       if (lane < kCandGran) gv = ld_wt(&wc->g[lane]);
       const bool stale = lane < kCandGran && (uint32_t)(gv >> 32) != (uint32_t)(tag >> 1);
       if (!__builtin_amdgcn_ballot_w64(stale)) break;
@@ -1391,6 +1458,33 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
   store_ctrl_wt(ctrl, zero_ctrl());
 }
 
+// A candidate's record payload, one 32-bit word per lane: lanes 0-23 the 12 pose doubles (low, high
+// halves), 24.. the (LED, blob) pairs, 56 the pair count.  One wave; ccorr: 2*kMaxMarkers LDS words.
+template <typename T>
+__device__ __forceinline__ uint32_t payload_word(const T* Pc, const uint32_t* ccorr, int np) {
+  const int lane = lane_id();
+  uint32_t pl = 0;
+  if (lane < 24) {
+    T pv = Pc[0];
+#pragma unroll
+    for (int q = 1; q < 12; ++q) pv = (lane >> 1) == q ? Pc[q] : pv;
+    const uint64_t bits = (uint64_t)__double_as_longlong((double)pv);
+    pl = (lane & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
+  } else if (lane < 24 + 2 * kMaxMarkers) {
+    pl = ccorr[lane - 24];
+  } else if (lane == 56) {
+    pl = (uint32_t)np;
+  }
+  return pl;
+}
+template <typename T, int MAXM>
+__device__ __forceinline__ uint32_t cand_payload(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
+                                                 const T* Pc, uint32_t* ccorr) {
+  int np = 0;
+  pose_pairs<T, MAXM>(fa, sc, tb, Pc, ccorr, &np);
+  return payload_word<T>(Pc, ccorr, np);
+}
+
 // LDS scratch of the resampling phase: scan partials, and per wave the staging of the scatter (the
 // wave's 64 kept particles as rows, and the slot -> owner-lane map of the current 64-slot chunk)
 template <typename T>
@@ -1407,7 +1501,9 @@ struct ResampleLds {
 // ---- stratified resampling of one block (PE:666-682) + count partials -> winner -> frame record.
 // wd: the thread's kept raw weight (0 for invalid lanes); P: its kept propagated particle when have_P,
 // else regenerated here from A (P_in unused).  Called by every thread; the caller checked c.done && c.accepted.
-template <typename T, int RNG, int MAXM, typename SP>
+// INLAUNCH (k_frame): the block also publishes its winner candidate and the last arriver finishes the
+// frame.  Otherwise (k_resample) the block only stores its count partial; k_resample_final finishes.
+template <typename T, int RNG, int MAXM, typename SP, bool INLAUNCH>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
@@ -1532,6 +1628,18 @@ __device__ __forceinline__ void resample_phase(
 
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 12, rt_now());
   __syncthreads();
+  if (!INLAUNCH) {  // block partial + the block argmax's kept pose (plain stores: the launch boundary
+                    // publishes them); a block without copies has no propagated row, k_resample_final regenerates
+    if (wv == 0) {
+      int bv = sh.c[0], bi = sh.ci[0];
+      for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
+      if (lane == 0) cpart[blk] = CountPart{bv, bi};
+      const int loc = bi - blk * kBlock;
+      if (lane < 12 && bv > 0) ((T*)(cand + blk))[lane] = sh.rows[loc >> 6][loc & 63].q[lane];
+      if (stamps && lane == 0) stamp_max(stamps, 5, rt_now());
+    }
+    return;
+  }
   if (wv == 1) {  // this block's winner candidate, in parallel with wave 0's arrival
     int cbv = sh.c[0], cbi = sh.ci[0];
     for (int w = 1; w < kWaves; ++w) cmb_max(cbv, cbi, sh.c[w], sh.ci[w]);
@@ -1546,20 +1654,7 @@ __device__ __forceinline__ void resample_phase(
     } else {
       make_particle<T, RNG, SP>(fa, sc, prior, cbi, kiter, Pc);
     }
-    int np = 0;
-    pose_pairs<T, MAXM>(fa, sc, tb, Pc, sh.ccorr, &np);
-    uint32_t pl = 0;
-    if (lane < 24) {
-      T pv = Pc[0];
-#pragma unroll
-      for (int q = 1; q < 12; ++q) pv = (lane >> 1) == q ? Pc[q] : pv;
-      const uint64_t bits = (uint64_t)__double_as_longlong((double)pv);
-      pl = (lane & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
-    } else if (lane < 24 + 2 * kMaxMarkers) {
-      pl = sh.ccorr[lane - 24];
-    } else if (lane == 56) {
-      pl = (uint32_t)np;
-    }
+    const uint32_t pl = cand_payload<T, MAXM>(fa, sc, tb, Pc, sh.ccorr);
     if (lane < kCandGran) st_wt(&cand[blk].g[lane], ((uint64_t)(uint32_t)seq << 32) | pl);
     if (stamps && lane == 0) stamp_max(stamps, 22, rt_now());
     return;
@@ -1632,24 +1727,132 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
   const Ctrl c = *ctrl;
-  if (!c.done) {  // speculative launch of an unfinished frame: report "not done"
-    if (blockIdx.x == 0 && threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
-    return;
-  }
-  stage_consts(fa, sc);  // visible after block_incl_sum's barrier (finalize below: same wave)
-  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-      wave_lds_sync();
-      finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
-    }
-    return;
-  }
+  // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
+  // k_resample_final writes the record
+  if (!c.done || !c.accepted) return;
+  stage_consts(fa, sc);  // visible after block_incl_sum's barrier
   const int slot = c.kept_slot;
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
-  resample_phase<T, RNG, MAXM, SP>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
+  resample_phase<T, RNG, MAXM, SP, false>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
                                mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+}
+
+// ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first
+// index, PE:685-686), its kept-iteration pose regenerated and paired once, then the frame record.  Also
+// reports an unfinished frame (speculative launch) and the re-init branch (PE:707-719).
+constexpr int kFinalBlock = 1024;
+template <typename T, int RNG, int MAXM, typename SP>
+__global__ __launch_bounds__(kFinalBlock) void k_resample_final(
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
+    const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
+    const double* __restrict__ mlpose, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the blob table
+  __shared__ LdsConst<T> sc;
+  __shared__ OutDev rec;
+  __shared__ int sv[kFinalBlock / 64], si[kFinalBlock / 64];
+  __shared__ uint32_t ccorr[2 * kMaxMarkers];
+  __shared__ T mk[kMaxMarkers];
+  __shared__ int rk[kMaxMarkers];
+  static_assert(kMaxMarkers <= kFinalBlock / 64, "one wave per marker");
+  const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+  if (stamps && threadIdx.x == 0) stamps[6] = rt_now();
+  // nothing below depends on the control record until the reduction is done: the partial, table and
+  // most-likely-pose loads go out together with it (on an unfinished frame they are simply unused)
+  const Ctrl c = *ctrl;
+  double ml = 0.0;
+  if (wv == 0 && lane < 12) ml = mlpose[lane];
+  stage_consts(fa, sc);
+  {
+    const uint4* s4 = (const uint4*)table;
+    uint4* d4 = (uint4*)smem;
+    const int n4 = (int)(BlobTable<T>::bytes(fa.B) / 16);
+    for (int q = (int)threadIdx.x; q < n4; q += kFinalBlock) d4[q] = s4[q];
+  }
+  int bv = -1, bi = 0x7fffffff;
+  {
+    const int nb = fa.nblk;
+    for (int base = (int)threadIdx.x; base < nb; base += 4 * kFinalBlock) {  // four predicated loads in flight
+      CountPart p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * kFinalBlock;
+        p[u] = i < nb ? cpart[i] : CountPart{-1, 0x7fffffff};
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) cmb_max(bv, bi, p[u].maxcount, p[u].idx);
+    }
+    wave_argmax(bv, bi);
+    if (lane == 0) {
+      sv[wv] = bv;
+      si[wv] = bi;
+    }
+  }
+  if (!c.done) {
+    if (threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
+    return;
+  }
+  __syncthreads();  // partials, table and constants
+  if (!c.accepted) {
+    if (wv == 0)
+      finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+    return;
+  }
+  // every wave: the winner (LDS broadcast) and its kept pose
+  bv = sv[0];
+  bi = si[0];
+  for (int w = 1; w < kFinalBlock / 64; ++w) cmb_max(bv, bi, sv[w], si[w]);
+  if (stamps && threadIdx.x == 0) stamps[24] = rt_now();
+  const bool marker_wave = wv < fa.M || wv == 0;  // wave-uniform
+  T Pc[12];
+  T u0 = (T)0, v0 = (T)0;
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  if (marker_wave) {
+  if (bv > 0) {  // staged by the winner's k_resample block
+    const T* row = (const T*)(cand + bi / kBlock);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) Pc[q] = row[q];
+  } else {  // every count is 0: the winner is particle 0 (PE:685), never propagated in k_resample
+    make_particle<T, RNG, SP>(fa, sc, prior, bi, c.kept_iter, Pc);
+  }
+  // wave j: marker j's nearest blob (pose_pairs' scan and tie rule, one marker per wave)
+  project_one<T>(sc, Pc, wv, u0, v0);
+  T best = inf_t<T>();
+  int arg = 0x7fffffff;
+  for (int i = lane; i < fa.B; i += 64) {
+    const BlobXY<T> p = tb.bxy[i];
+    const int o = tb.orig[i];
+    const T dx = p.x - u0;
+    const T dy = p.y - v0;
+    const T d = fmadd(dx, dx, dy * dy);
+    if (d < best || (d == best && o < arg)) {
+      best = d;
+      arg = o;
+    }
+  }
+  wave_argmin(best, arg);
+  if (lane == 0) {
+    mk[wv] = best;
+    rk[wv] = arg == 0x7fffffff ? 0 : arg;
+  }
+  }
+  if (stamps && threadIdx.x == 0) stamps[25] = rt_now();
+  __syncthreads();  // the per-marker minima
+  if (wv != 0) return;
+  T m[MAXM];
+  int r[MAXM];
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    m[j] = j < fa.M ? mk[j] : inf_t<T>();
+    r[j] = j < fa.M ? rk[j] : 0;
+  }
+  const int np = pairs_from_minima<T, MAXM>(fa, tb, m, r, u0, v0, ccorr);  // wave 0 projected marker 0
+  const uint32_t pl = payload_word<T>(Pc, ccorr, np);
+  if (stamps && lane == 0) stamps[26] = rt_now() + (uint64_t)(pl == 12345u ? 1 : 0);
+  finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, bi, cand, mlpose, rec, out, 2 * seq + 1, stamps, true, pl,
+                                   ml);
+  if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
 // ---- the whole frame in ONE cooperative launch (every block co-resident, checked by the host): the
@@ -1773,7 +1976,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   }
   const BlockScan bs = fsh.bs[kslot];
   const GroupScan gs = fsh.gs;
-  resample_phase<T, RNG, MAXM, SP>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+  resample_phase<T, RNG, MAXM, SP, true>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
                                mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
 }
 

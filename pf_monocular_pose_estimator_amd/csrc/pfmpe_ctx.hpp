@@ -240,6 +240,11 @@ struct Seq {
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
                          c->d_stamps);
     }));
+    RET(launch(c, PFMPE_K_FINAL, [&] {
+      hipLaunchKernelGGL((k_resample_final<T, RNG, MAXM, SP>), dim3(1), dim3(kFinalBlock), BlobTable<T>::bytes(fa.B),
+                         c->stream, fa, c->d_ctrl,
+                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps);
+    }));
     RET(wait_frame(c));
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;

@@ -579,7 +579,8 @@ int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
 }
 
 const char* pfmpe_kernel_name(int kernel) {
-  static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux", "k_frame", "k_roi"};
+  static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux", "k_frame", "k_roi",
+                                                 "k_resample_final"};
   return (kernel >= 0 && kernel < PFMPE_K_COUNT) ? names[kernel] : "?";
 }
 
