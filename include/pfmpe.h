@@ -162,6 +162,48 @@ typedef struct {
 } pfmpe_roi_out;
 int pfmpe_predict_roi(pfmpe_ctx* ctx, const pfmpe_roi_in* in, pfmpe_roi_out* out);
 
+/* ------------------------------------------------- brute-force P3P (re)initialisation (§8f row 2) */
+/* PoseEstimator::initialise (PE:1503-1786) for the particle-filter configuration, run when the track is
+ * lost (it_since_initialized_ < 1, PE:128-205).  Blobs are image_points_ (undistorted px).  Stages:
+ *   1. histogram (PE:1526-1716, device): for every 3-blob combination passing the spread filter
+ *      (threshDist, >= 5 blobs near the centroid) x every ordered 3-marker permutation, P3P
+ *      (p3p.cpp:65-292) gives 4 poses; each finite, non-repeated pose back-projects the unused markers
+ *      through H.inverse() and, when at least one unused blob lies within tol of its nearest projection,
+ *      the 3 P3P pairs and every such (blob, nearest marker) pair are counted;
+ *   2. candidate correspondence vectors (correspondencesFromHistogram PE:1134-1288, host);
+ *   3. checkCorrespondences of every candidate (PE:1312-1501; P3P over each 3-subset, device), the
+ *      particle seeding and the fill loop (PE:1429-1437, 1755-1760), predicted_pose_ by
+ *      computeTransformation (PE:2139-2161, host) for the first match.
+ * tol = the context's params.tol (back_projection_pixel_tolerance_, shared with the PF score). */
+typedef struct {
+  double certainty_threshold;  /* certainty_threshold_ (PE:1411), README default 1                    */
+  double valid_corr_threshold; /* valid_correspondence_threshold_ (PE:1477), README default 0.5        */
+  int32_t n_particles;         /* N_Particle; 0 = the context's current N (max_particles if none)      */
+  int32_t max_candidates;      /* cap on correspondence vectors (PFMPE_E_CAP beyond it); default 4096  */
+} pfmpe_init_params;
+typedef struct {
+  int32_t found;            /* initialise() == 1; the particle set is then seeded (see below)       */
+  int32_t flag_fail;        /* 0 when found, else the last PubData.Flag_Fail code initialise wrote:
+                               10 too few blobs, 12 empty histogram, 11 no candidate, 6 too few
+                               correspondences, 9 P3P failed, 7 / 8 validity ratio; -1 none          */
+  int32_t n_estimates;      /* P3P poses stored into PoseParticle (NumberOfP3PEstimation - 1)        */
+  int32_t n_candidates;     /* correspondence vectors from the histogram                            */
+  int32_t first_match;      /* candidate giving correspondences_ / predicted_pose_ (-1: none)      */
+  int32_t n_corr;           /* rows of correspondences_                                             */
+  uint32_t corr[2 * PFMPE_MAX_MARKERS]; /* (LED, blob) 1-based pairs                                 */
+  double predicted_pose[12];/* predicted_pose_ (computeTransformation of the mean re-projections)   */
+  uint64_t hist_total;      /* sum of the histogram                                                 */
+} pfmpe_init_out;
+void pfmpe_default_init_params(pfmpe_init_params* p);
+/* Stage 1 alone: hist (B x M uint32, row-major: hist[blob * M + marker]).  3 <= B <= max_blobs. */
+int pfmpe_p3p_histogram(pfmpe_ctx* ctx, const double* blobs, int B, uint32_t* hist);
+/* The whole initialise().  On success (out->found) the context's particle set becomes PoseParticle
+ * (newPoseEstimation_Vec = PoseParticle, PE:191): slot N-k holds the k-th stored P3P pose (k = 1..K),
+ * slots below repeat them with period K (the fill loop), and slot 0 keeps the resident set's slot 0
+ * (identity if there is none) unless K >= N.  hist (optional, B x M) receives stage 1's histogram. */
+int pfmpe_initialise(pfmpe_ctx* ctx, const double* blobs, int B, const pfmpe_init_params* params,
+                     pfmpe_init_out* out, uint32_t* hist);
+
 /* getPoseParticles (PE:917, which = 0: kept propagated set of the last step) and getResampledParticles
  * (PE:923, which = 1: current prior).  N x 12 doubles. */
 int pfmpe_get_particles(pfmpe_ctx* ctx, int which, double* out);
@@ -195,7 +237,9 @@ enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduc
        PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one launch              */
        PFMPE_K_ROI = 4,       /* k_roi + k_roi_final (pfmpe_predict_roi)             */
        PFMPE_K_FINAL = 5,     /* k_resample_final: winner + frame record (one block) */
-       PFMPE_K_COUNT = 6 };
+       PFMPE_K_P3P_HIST = 6,  /* k_p3p_hist: initialisation histogram                */
+       PFMPE_K_P3P_CHECK = 7, /* k_p3p_check: checkCorrespondences of all candidates */
+       PFMPE_K_COUNT = 8 };
 int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
 int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
 const char* pfmpe_kernel_name(int kernel);

@@ -56,6 +56,23 @@ class OrcFrameOut(C.Structure):
         }
 
 
+class OrcInitParams(C.Structure):
+    _fields_ = [("tol", C.c_double), ("certainty_threshold", C.c_double), ("valid_corr_threshold", C.c_double),
+                ("use_pf", C.c_int), ("max_candidates", C.c_int)]
+
+
+class OrcInitOut(C.Structure):
+    _fields_ = [("found", C.c_int), ("flag_fail", C.c_int), ("n_estimates", C.c_int), ("n_candidates", C.c_int),
+                ("first_match", C.c_int), ("n_corr", C.c_int), ("corr", C.c_uint32 * 32),
+                ("predicted_pose", C.c_double * 12), ("hist_total", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {"found": self.found, "flag_fail": self.flag_fail, "n_estimates": self.n_estimates,
+                "n_candidates": self.n_candidates, "first_match": self.first_match,
+                "pairs": np.array(self.corr[: 2 * self.n_corr], dtype=np.uint32).reshape(-1, 2),
+                "predicted_pose": np.array(self.predicted_pose), "hist_total": self.hist_total}
+
+
 _lib = None
 
 
@@ -102,6 +119,18 @@ def load() -> C.CDLL:
     lib.orc_predict_roi.restype = C.c_int
     lib.orc_predict_roi.argtypes = [C.c_int, C.c_int, dp, dp, dp, dp, dp, dp, dp, C.c_int, C.c_int, C.c_int,
                                     C.POINTER(C.c_int), dp]
+    u32p = C.POINTER(C.c_uint32)
+    lib.orc_image_vectors.restype = C.c_int
+    lib.orc_image_vectors.argtypes = [dp, C.c_int, dp, dp]
+    lib.orc_p3p.restype = C.c_int
+    lib.orc_p3p.argtypes = [dp, dp, dp]
+    lib.orc_inverse44.restype = None
+    lib.orc_inverse44.argtypes = [dp, dp]
+    lib.orc_init_histogram.restype = C.c_int
+    lib.orc_init_histogram.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.c_double, u32p]
+    lib.orc_initialise.restype = C.c_int
+    lib.orc_initialise.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.POINTER(OrcInitParams), C.c_int, u32p, u32p,
+                                   dp, C.POINTER(OrcInitOut)]
     _lib = lib
     return lib
 
@@ -264,3 +293,61 @@ def predict_roi(markers, K, D, prior, cam_move_inv, prediction, predicted_pose, 
                            _p(_d(cam_move_inv).reshape(12)), _p(_d(prediction).reshape(12)),
                            _p(_d(predicted_pose).reshape(12)), image_w, image_h, border, roi, _p(bbox))
     return list(roi), bbox
+
+
+# ------------------------------------------------------------------ brute-force P3P initialisation
+def image_vectors(K, blobs):
+    b = _d(blobs).reshape(-1, 2)
+    out = np.zeros((b.shape[0], 3))
+    load().orc_image_vectors(_p(_d(K).reshape(9)), b.shape[0], _p(b), _p(out))
+    return out
+
+
+def p3p(feature_vectors, world_points):
+    """P3P::computePoses on rows = the three unit feature vectors / world points -> (rc, 4 x 12)."""
+    sol = np.zeros((4, 12))
+    rc = load().orc_p3p(_p(_d(feature_vectors).reshape(9)), _p(_d(world_points).reshape(9)), _p(sol))
+    return rc, sol
+
+
+def inverse44(sol12):
+    out = np.zeros(16)
+    load().orc_inverse44(_p(_d(sol12).reshape(12)), _p(out))
+    return out.reshape(4, 4)
+
+
+def init_histogram(markers, K, blobs, tol=5.0):
+    m = _d(markers).reshape(-1, 3)
+    b = _d(blobs).reshape(-1, 2)
+    h = np.zeros((b.shape[0], m.shape[0]), dtype=np.uint32)
+    rc = load().orc_init_histogram(m.shape[0], _p(m), _p(_d(K).reshape(9)), b.shape[0], _p(b), tol,
+                                   h.ctypes.data_as(C.POINTER(C.c_uint32)))
+    if rc != 0:
+        raise ValueError("orc_init_histogram: bad sizes")
+    return h
+
+
+def initialise(markers, K, blobs, n_particles, particles=None, tol=5.0, certainty_threshold=1.0,
+               valid_corr_threshold=0.5, use_pf=True, max_candidates=65536, hist=None):
+    """PoseEstimator::initialise (PE:1503-1786) -> (out dict, hist (B x M), particles (N x 12)).
+    `particles` is PoseParticle before the call (default: identity poses); `hist` overrides the
+    histogram stage."""
+    m = _d(markers).reshape(-1, 3)
+    b = _d(blobs).reshape(-1, 2)
+    M, B = m.shape[0], b.shape[0]
+    if particles is None:
+        particles = np.tile(np.eye(4)[:3].reshape(12), (n_particles, 1))
+    pp = np.array(_d(particles).reshape(n_particles, 12))
+    hout = np.zeros((B, M), dtype=np.uint32)
+    hin = None
+    if hist is not None:
+        hin = np.ascontiguousarray(hist, dtype=np.uint32).reshape(B, M)
+    prm = OrcInitParams(tol, certainty_threshold, valid_corr_threshold, 1 if use_pf else 0, max_candidates)
+    out = OrcInitOut()
+    u32 = C.POINTER(C.c_uint32)
+    rc = load().orc_initialise(M, _p(m), _p(_d(K).reshape(9)), B, _p(b), C.byref(prm), n_particles,
+                               hin.ctypes.data_as(u32) if hin is not None else u32(), hout.ctypes.data_as(u32),
+                               _p(pp), C.byref(out))
+    if rc != 0:
+        raise RuntimeError(f"orc_initialise failed: {rc}")
+    return out.as_dict(), hout, pp

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
-K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_COUNT = 0, 1, 2, 3, 4, 5, 6
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_COUNT = 0, 1, 2, 3, 4, 5, 6, 7, 8
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "pfmpe_step", "pfmpe_step_batch", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
-    "pfmpe_predict_roi",
+    "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
 )
 
 
@@ -66,6 +66,24 @@ class RoiIn(C.Structure):
 class RoiOut(C.Structure):
     _fields_ = [("x", C.c_int32), ("y", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
                 ("bbox", C.c_double * 4)]
+
+
+class InitParams(C.Structure):
+    _fields_ = [("certainty_threshold", C.c_double), ("valid_corr_threshold", C.c_double),
+                ("n_particles", C.c_int32), ("max_candidates", C.c_int32)]
+
+
+class InitOut(C.Structure):
+    _fields_ = [("found", C.c_int32), ("flag_fail", C.c_int32), ("n_estimates", C.c_int32),
+                ("n_candidates", C.c_int32), ("first_match", C.c_int32), ("n_corr", C.c_int32),
+                ("corr", C.c_uint32 * (2 * MAX_MARKERS)), ("predicted_pose", C.c_double * 12),
+                ("hist_total", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {"found": self.found, "flag_fail": self.flag_fail, "n_estimates": self.n_estimates,
+                "n_candidates": self.n_candidates, "first_match": self.first_match,
+                "pairs": np.array(self.corr[: 2 * self.n_corr], dtype=np.uint32).reshape(-1, 2),
+                "predicted_pose": np.array(self.predicted_pose), "hist_total": self.hist_total}
 
 
 class FrameOut(C.Structure):
@@ -128,6 +146,9 @@ def load() -> C.CDLL:
         "pfmpe_host_ref_uniform": (D, [C.c_uint32, U64, D, D]),
         "pfmpe_host_philox": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
         "pfmpe_predict_roi": (I, [P, C.POINTER(RoiIn), C.POINTER(RoiOut)]),
+        "pfmpe_default_init_params": (None, [C.POINTER(InitParams)]),
+        "pfmpe_p3p_histogram": (I, [P, dp, I, C.POINTER(C.c_uint32)]),
+        "pfmpe_initialise": (I, [P, dp, I, C.POINTER(InitParams), C.POINTER(InitOut), C.POINTER(C.c_uint32)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -164,7 +185,9 @@ class Engine:
         if rc != OK:
             raise PFError(rc, "pfmpe_create failed (no HIP device?)")
         self.state_dtype = state_dtype
+        self.max_particles = max_particles
         self.N = 0
+        self.M = 0
 
     def close(self):
         if self.ctx:
@@ -189,6 +212,7 @@ class Engine:
             dga = np.ascontiguousarray(downgrade, dtype=np.uint8)
             dg = dga.ctypes.data_as(C.POINTER(C.c_uint8))
         self._chk(self.lib.pfmpe_set_model(self.ctx, _dptr(m), m.shape[0], _dptr(k), dg))
+        self.M = m.shape[0]
 
     def set_params(self, params: Params):
         self._chk(self.lib.pfmpe_set_params(self.ctx, C.byref(params)))
@@ -263,6 +287,33 @@ class Engine:
         ro = RoiOut()
         self._chk(self.lib.pfmpe_predict_roi(self.ctx, C.byref(ri), C.byref(ro)))
         return {"roi": [ro.x, ro.y, ro.width, ro.height], "bbox": np.array(list(ro.bbox))}
+
+    def p3p_histogram(self, blobs) -> np.ndarray:
+        """Stage 1 of initialise (PE:1526-1716): the B x M correspondence histogram (uint32)."""
+        b = np.ascontiguousarray(blobs, dtype=np.float64).reshape(-1, 2)
+        h = np.zeros((b.shape[0], self.M), dtype=np.uint32)
+        self._chk(self.lib.pfmpe_p3p_histogram(self.ctx, _dptr(b), b.shape[0], h.ctypes.data_as(C.POINTER(C.c_uint32))))
+        return h
+
+    def initialise(self, blobs, n_particles=0, certainty_threshold=1.0, valid_corr_threshold=0.5,
+                   max_candidates=4096):
+        """PoseEstimator::initialise (PE:1503-1786) -> (out dict, histogram).  On success the context's
+        particle set is the seeded PoseParticle set (self.N = n_particles)."""
+        b = np.ascontiguousarray(blobs, dtype=np.float64).reshape(-1, 2)
+        ip = InitParams()
+        self.lib.pfmpe_default_init_params(C.byref(ip))
+        ip.certainty_threshold = certainty_threshold
+        ip.valid_corr_threshold = valid_corr_threshold
+        ip.n_particles = int(n_particles)
+        ip.max_candidates = int(max_candidates)
+        out = InitOut()
+        h = np.zeros((b.shape[0], self.M), dtype=np.uint32)
+        self._chk(self.lib.pfmpe_initialise(self.ctx, _dptr(b), b.shape[0], C.byref(ip), C.byref(out),
+                                            h.ctypes.data_as(C.POINTER(C.c_uint32))))
+        d = out.as_dict()
+        if d["found"]:
+            self.N = int(n_particles) if n_particles else (self.N or self.max_particles)
+        return d, h
 
     def get_particles(self, which: int) -> np.ndarray:
         out = np.empty((self.N, 12), dtype=np.float64)

@@ -59,6 +59,8 @@ struct pfmpe_ctx {
   Cand* d_cand = nullptr;          // per-block winner candidates
   double* d_mlpose = nullptr;      // most likely pose (12)
   double* d_roi = nullptr;         // ROI box [4] + per-block partials
+  unsigned char* d_init = nullptr; // initialisation scratch (pfmpe_init.hip), grown on demand
+  size_t init_cap = 0;
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
   bool fused = true;               // PFMPE_OPT_FUSED

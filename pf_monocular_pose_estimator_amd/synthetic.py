@@ -255,3 +255,23 @@ def make_stream(cfg: StreamConfig, n_frames: int, t0: float = 0.5) -> Stream:
         Pm = se3_exp(delta)
         st.frames.append(Frame(f, t, T, to12(Tc), to12(Tc @ Pm), to12(Pm), blobs_for_frame(cfg, T, f, markers), dt))
     return st
+
+
+def init_blobs(M: int = 5, n_out: int = 3, seed: int = 0, noise_px: float = 0.0, t: float = 0.5,
+               near: int = 0):
+    """Detections of a track-loss frame for the brute-force initialisation (PE:1503): every marker at
+    truth_pose(t) (+ N(0, noise_px)), `near` outliers 1-5 px from true blobs, `n_out` uniform outliers,
+    shuffled and rounded through float32 like detector output.  Returns (blobs B x 2, truth 4x4)."""
+    rng = np.random.default_rng(5000 + seed)
+    T = truth_pose(t)
+    markers = markers_for(M)
+    px = project(K_README, T, markers) + (rng.normal(0.0, noise_px, size=(M, 2)) if noise_px > 0 else 0.0)
+    blobs = list(px)
+    for _ in range(near):
+        base = px[int(rng.integers(0, M))]
+        blobs.append(base + rng.integers(1, 6, size=2) * rng.choice([-1, 1], size=2))
+    for _ in range(n_out):
+        blobs.append(np.array([rng.uniform(0, IMAGE_W), rng.uniform(0, IMAGE_H)]))
+    blobs = np.array(blobs)
+    rng.shuffle(blobs)
+    return blobs.astype(np.float32).astype(np.float64), T
