@@ -179,7 +179,7 @@ typedef struct {
   double certainty_threshold;  /* certainty_threshold_ (PE:1411), README default 1                    */
   double valid_corr_threshold; /* valid_correspondence_threshold_ (PE:1477), README default 0.5        */
   int32_t n_particles;         /* N_Particle; 0 = the context's current N (max_particles if none)      */
-  int32_t max_candidates;      /* cap on correspondence vectors (PFMPE_E_CAP beyond it); default 4096  */
+  int32_t max_candidates;      /* cap on correspondence vectors (PFMPE_E_CAP beyond it); default 2^20  */
 } pfmpe_init_params;
 typedef struct {
   int32_t found;            /* initialise() == 1; the particle set is then seeded (see below)       */

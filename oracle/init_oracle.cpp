@@ -104,7 +104,7 @@ void solve_quartic(const double f[5], double roots[4]) {
 // fv / wp: the three feature vectors / world points (fv[k], wp[k] = column k).  Returns -1 when the
 // world points are collinear, else 0 with four [R|C] solutions (camera orientation and position in
 // the world frame).
-int p3p(const double fv[3][3], const double wp[3][3], Pose34 sol[4]) {
+int p3p(const double fv[3][3], const double wp[3][3], Pose34 sol[4], double* roots_out = nullptr) {
   double P1[3], P2[3], P3[3];
   std::memcpy(P1, wp[0], sizeof(P1));
   std::memcpy(P2, wp[1], sizeof(P2));
@@ -205,6 +205,7 @@ int p3p(const double fv[3][3], const double wp[3][3], Pose34 sol[4]) {
            p_2_pw2 * f_1_pw2 * p_1_pw2 + f_2_pw2 * p_2_pw2 * d_12_pw2 * b_pw2;
   double roots[4];
   solve_quartic(fac, roots);
+  if (roots_out) std::memcpy(roots_out, roots, sizeof(roots));
 
   for (int i = 0; i < 4; ++i) {
     const double cot_alpha = (-f_1 * p_1 / f_2 - roots[i] * p_2 + d_12 * b) / (-f_1 * roots[i] * p_2 / f_2 + p_1 - d_12);
@@ -369,9 +370,21 @@ std::vector<int> permutations3(int n) {
 }
 
 // ------------------------------------------------------------------ histogram (PE:1526-1716)
+// hist: the reference's histogram.  lo / hi (optional): bounds that every implementation whose fp64
+// arithmetic differs from this one only at the ulp level must fall between.  Three reference decisions
+// hinge on exact floating-point equality or a threshold and are "fragile" when their margin is at the
+// ulp level: the repeated-solution skip (two roots within 64 ulp: a complex-conjugate pair whose real
+// parts come out equal or not depending on the last bits of the libm calls inside std::complex pow),
+// a root at |cos theta| = 1 (isFinite), and a blob at the tol gate or tied between two projections.
+// A fragile contribution goes to hi only; everything else to both.  *unbounded counts fragile
+// isFinite cases (their contribution cannot be bounded from here).
 void histogram(int M, const double* markers, const double* K, int B, const double* blobs, double tol,
-               uint32_t* hist /* B x M, row-major */) {
+               uint32_t* hist /* B x M, row-major */, uint32_t* lo = nullptr, uint32_t* hi = nullptr,
+               int* unbounded = nullptr) {
   std::memset(hist, 0, sizeof(uint32_t) * (size_t)B * M);
+  if (lo) std::memset(lo, 0, sizeof(uint32_t) * (size_t)B * M);
+  if (hi) std::memset(hi, 0, sizeof(uint32_t) * (size_t)B * M);
+  if (unbounded) *unbounded = 0;
   std::vector<double> iv;
   image_vectors(K, B, blobs, iv);
   const std::vector<int> cmb = combinations3(B);
@@ -379,6 +392,7 @@ void histogram(int M, const double* markers, const double* K, int B, const doubl
   const double threshDist = 10000 * 100, threshDist2 = 10000 * 100;
   std::vector<double> un_im;
   std::vector<int> un_im_idx;
+  std::vector<int> pair_obj(B), state(B);
   for (size_t ci = 0; ci < cmb.size() / 3; ++ci) {
     const int* s = &cmb[3 * ci];
     double fv[3][3];
@@ -413,45 +427,74 @@ void histogram(int M, const double* markers, const double* K, int B, const doubl
       for (int k = 0; k < 3; ++k)
         for (int q = 0; q < 3; ++q) wp[k][q] = markers[3 * p[k] + q];
       Pose34 sol[4];
-      if (p3p(fv, wp, sol) != 0) continue;
+      double roots[4];
+      if (p3p(fv, wp, sol, roots) != 0) continue;
       int un_obj[16];
       int nuo = 0;
       for (int ll = 0; ll < M; ++ll)
         if (ll != p[0] && ll != p[1] && ll != p[2]) un_obj[nuo++] = ll;
       for (int k = 0; k < 4; ++k) {
+        bool repeated = false, frag_sol = false;
         if (k > 0) {  // (solutions(k) - solutions(k-1)).all() == 0  <=>  some entry difference is 0
-          bool any_zero = false;
           for (int q = 0; q < 12; ++q)
-            if (sol[k].a[q] - sol[k - 1].a[q] == 0) any_zero = true;
-          if (any_zero) continue;
+            if (sol[k].a[q] - sol[k - 1].a[q] == 0) repeated = true;
+          const double a = roots[k], b = roots[k - 1];
+          frag_sol = std::fabs(a - b) <= 64 * std::numeric_limits<double>::epsilon() * std::max(std::fabs(a), std::fabs(b));
         }
-        if (!is_finite34(sol[k])) continue;
+        if (repeated && !frag_sol) continue;
+        if (!is_finite34(sol[k])) {
+          if (unbounded && std::fabs(1.0 - std::fabs(roots[k])) < 1e-9) ++*unbounded;
+          continue;
+        }
+        const bool counted_ref = !repeated;  // the reference's own decision
         double inv[16];
         inverse44(sol[k], inv);
         double proj[16][2];
         for (int m = 0; m < nuo; ++m) project44(K, inv, markers + 3 * un_obj[m], proj[m]);
         // calculateMinDistancesAndPairs(unused image points, back-projected unused markers)
-        int counted = 0;
-        int pair_obj[1024];
-        bool within[1024];
+        int n_in = 0, n_in_strict = 0;
         for (int a = 0; a < nui; ++a) {
-          double mind = INFINITY;
+          double mind = INFINITY, second = INFINITY;
           int pr = 0;
           for (int m = 0; m < nuo; ++m) {
             const double dsq = sqdist2(&un_im[2 * a], proj[m]);
             if (dsq < mind) {
+              second = mind;
               mind = dsq;
               pr = m + 1;
+            } else if (dsq < second) {
+              second = dsq;
             }
           }
-          within[a] = std::sqrt(mind) < tol;
+          const double d = std::sqrt(mind);
+          const bool in = d < tol;
+          const bool frag = std::fabs(d - tol) <= 1e-9 * tol || (second - mind <= 1e-9 * mind && d < tol * (1 + 1e-9));
           pair_obj[a] = pr;
-          if (within[a]) counted++;
+          state[a] = in ? (frag ? 1 : 2) : (frag ? 1 : 0);  // 0 out, 1 fragile, 2 in
+          if (in) n_in++;
+          if (state[a] == 2) n_in_strict++;
         }
-        if (counted > 0) {
+        if (counted_ref && n_in > 0) {
           for (int mm = 0; mm < 3; ++mm) hist[(size_t)s[mm] * M + p[mm]] += 1;
           for (int a = 0; a < nui; ++a)
-            if (within[a]) hist[(size_t)un_im_idx[a] * M + un_obj[pair_obj[a] - 1]] += 1;
+            if (state[a] == 2 || (state[a] == 1 && std::sqrt(sqdist2(&un_im[2 * a], proj[pair_obj[a] - 1])) < tol))
+              hist[(size_t)un_im_idx[a] * M + un_obj[pair_obj[a] - 1]] += 1;
+        }
+        if (!lo || !hi) continue;
+        bool any_frag = false;
+        for (int a = 0; a < nui; ++a) any_frag = any_frag || state[a] == 1;
+        if (n_in_strict > 0 || any_frag) {  // the combination's 3 pairs: certain iff a certain blob counts
+          const bool certain = !frag_sol && n_in_strict > 0;
+          for (int mm = 0; mm < 3; ++mm) {
+            hi[(size_t)s[mm] * M + p[mm]] += 1;
+            if (certain) lo[(size_t)s[mm] * M + p[mm]] += 1;
+          }
+          for (int a = 0; a < nui; ++a) {
+            if (state[a] == 0 || pair_obj[a] == 0) continue;
+            const size_t e = (size_t)un_im_idx[a] * M + un_obj[pair_obj[a] - 1];
+            hi[e] += 1;
+            if (certain && state[a] == 2) lo[e] += 1;
+          }
         }
       }
     }
@@ -666,6 +709,14 @@ int orc_init_histogram(int M, const double* markers, const double* K, int B, con
 // initialise() (PE:1503-1786) for the particle-filter configuration.
 //   particles: N x 12 in/out (PoseParticle: slots the reference writes are overwritten, the rest kept)
 //   hist_in:   optional histogram to use instead of computing one (isolates the post-histogram stages)
+// the histogram plus its fragility bounds lo <= any ulp-level reimplementation <= hi (see histogram())
+int orc_init_histogram_bounds(int M, const double* markers, const double* K, int B, const double* blobs, double tol,
+                              uint32_t* hist, uint32_t* lo, uint32_t* hi, int* unbounded) {
+  if (B < 3 || B > 1024 || M < 3 || M > 16) return -1;
+  histogram(M, markers, K, B, blobs, tol, hist, lo, hi, unbounded);
+  return 0;
+}
+
 int orc_initialise(int M, const double* markers, const double* K, int B, const double* blobs,
                    const OrcInitParams* prm, int N_particle, const uint32_t* hist_in, uint32_t* hist_out,
                    double* particles, OrcInitOut* out) {

@@ -128,6 +128,9 @@ def load() -> C.CDLL:
     lib.orc_inverse44.argtypes = [dp, dp]
     lib.orc_init_histogram.restype = C.c_int
     lib.orc_init_histogram.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.c_double, u32p]
+    lib.orc_init_histogram_bounds.restype = C.c_int
+    lib.orc_init_histogram_bounds.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.c_double, u32p, u32p, u32p,
+                                              C.POINTER(C.c_int)]
     lib.orc_initialise.restype = C.c_int
     lib.orc_initialise.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.POINTER(OrcInitParams), C.c_int, u32p, u32p,
                                    dp, C.POINTER(OrcInitOut)]
@@ -325,6 +328,21 @@ def init_histogram(markers, K, blobs, tol=5.0):
     if rc != 0:
         raise ValueError("orc_init_histogram: bad sizes")
     return h
+
+
+def init_histogram_bounds(markers, K, blobs, tol=5.0):
+    """(hist, lo, hi, unbounded): the reference histogram and the band any ulp-level reimplementation must
+    land in (fragile decisions: repeated-solution skip between near-equal roots, the tol gate, ties)."""
+    m = _d(markers).reshape(-1, 3)
+    b = _d(blobs).reshape(-1, 2)
+    hs = [np.zeros((b.shape[0], m.shape[0]), dtype=np.uint32) for _ in range(3)]
+    ub = C.c_int()
+    u32 = C.POINTER(C.c_uint32)
+    rc = load().orc_init_histogram_bounds(m.shape[0], _p(m), _p(_d(K).reshape(9)), b.shape[0], _p(b), tol,
+                                          *[h.ctypes.data_as(u32) for h in hs], C.byref(ub))
+    if rc != 0:
+        raise ValueError("orc_init_histogram_bounds: bad sizes")
+    return hs[0], hs[1], hs[2], ub.value
 
 
 def initialise(markers, K, blobs, n_particles, particles=None, tol=5.0, certainty_threshold=1.0,

@@ -296,7 +296,7 @@ class Engine:
         return h
 
     def initialise(self, blobs, n_particles=0, certainty_threshold=1.0, valid_corr_threshold=0.5,
-                   max_candidates=4096):
+                   max_candidates=1 << 20):
         """PoseEstimator::initialise (PE:1503-1786) -> (out dict, histogram).  On success the context's
         particle set is the seeded PoseParticle set (self.N = n_particles)."""
         b = np.ascontiguousarray(blobs, dtype=np.float64).reshape(-1, 2)

@@ -549,11 +549,29 @@ int candidates(pfmpe_ctx* c, int B, int M, const uint32_t* hist, int max_cand,
   double sum = 0;
   for (int i = 0; i < N; ++i) sum += vp[i];
   for (int i = 0; i < N; ++i) vp[i] = vp[i] / sum;
-  for (int bb = 0; bb < N; ++bb) {  // repeated std::max_element (first maximum), picked entry zeroed
-    int row = 0;
-    for (int i = 1; i < N; ++i)
-      if (vp[row] < vp[i]) row = i;
-    vp[row] = 0;
+  // N rounds of std::max_element (first maximum) with the picked entry zeroed (PE:1256-1260).  Without
+  // NaNs that is: the positive entries by (value desc, index asc), then index 0 (all zero by then) for
+  // each entry that was not positive.  A NaN (sum 0 or inf) falls back to the literal O(N^2) rounds.
+  std::vector<int> picks;
+  picks.reserve(N);
+  bool has_nan = false;
+  for (int i = 0; i < N; ++i) has_nan = has_nan || !(vp[i] == vp[i]);
+  if (!has_nan) {
+    for (int i = 0; i < N; ++i)
+      if (vp[i] > 0) picks.push_back(i);
+    std::stable_sort(picks.begin(), picks.end(), [&](int x, int y) { return vp[x] > vp[y]; });
+    while ((int)picks.size() < N) picks.push_back(0);
+  } else {
+    for (int bb = 0; bb < N; ++bb) {
+      int row = 0;
+      for (int i = 1; i < N; ++i)
+        if (vp[row] < vp[i]) row = i;
+      vp[row] = 0;
+      picks.push_back(row);
+    }
+  }
+  for (int bb = 0; bb < N; ++bb) {
+    const int row = picks[bb];
     const int* det = &comb[(size_t)row * M];
     bool amb = false;  // checkAmbiguity (PE:2447-2458)
     for (int i = 0; i < M && !amb; ++i)
@@ -647,7 +665,7 @@ void pfmpe_default_init_params(pfmpe_init_params* p) {
   p->certainty_threshold = 1.0;   // README.md:245, launch file README.md:340
   p->valid_corr_threshold = 0.5;  // README.md:249
   p->n_particles = 0;
-  p->max_candidates = 4096;
+  p->max_candidates = 1 << 20;
 }
 
 int pfmpe_p3p_histogram(pfmpe_ctx* c, const double* blobs, int B, uint32_t* hist) {
@@ -675,7 +693,7 @@ int pfmpe_initialise(pfmpe_ctx* c, const double* blobs, int B, const pfmpe_init_
   pfmpe_init_params p;
   pfmpe_default_init_params(&p);
   if (prm) p = *prm;
-  if (p.max_candidates <= 0) p.max_candidates = 4096;
+  if (p.max_candidates <= 0) p.max_candidates = 1 << 20;
   const int N = p.n_particles > 0 ? p.n_particles : (c->has_prior ? c->N : c->max_particles);
   if (N > c->max_particles) return fail(c, PFMPE_E_CAP, "initialise: n_particles exceeds max_particles");
   std::memset(out, 0, sizeof(*out));
