@@ -204,6 +204,43 @@ int pfmpe_p3p_histogram(pfmpe_ctx* ctx, const double* blobs, int B, uint32_t* hi
 int pfmpe_initialise(pfmpe_ctx* ctx, const double* blobs, int B, const pfmpe_init_params* params,
                      pfmpe_init_out* out, uint32_t* hist);
 
+/* ---------------------------------------- configuration files and recorded streams (§8f row 3) */
+/* Host-only (no GPU): pfmpe_io.cpp.  The reference reads these through ROS (rosparam / getParam /
+ * dynamic_reconfigure, pf_mpe/src/monocular_pose_estimator.cpp:81-126, 479-527) and the CameraInfo topic.
+ * Marker YAML (README.md:95-117): `marker_positions:` followed by a list of {x, y, z} maps (block or flow
+ * style).  Writes min(count, max_markers) rows of xyz; returns the number of markers, or < 0. */
+int pfmpe_parse_marker_yaml(const char* text, double* xyz, int max_markers);
+/* The PF / initialisation / marker-split parameters of a ROS launch file (<param name=.. value=../>,
+ * pf_mpe/launch/<name>.launch): the names dynamicParametersCallback copies into PoseEstimator.  Absent names
+ * keep the defaults of pfmpe_default_launch_config (the engine's defaults).  Returns how many names
+ * were recognised. */
+typedef struct {
+  pfmpe_params pf;                       /* back_projection_pixel_tolerance(_PF), min/maxAngularNoise,
+                                            min/maxTransitionNoise                                       */
+  pfmpe_init_params init;                /* certainty_threshold, valid_correspondence_threshold, N_Particle */
+  int32_t num_objects;                   /* numUAV                                                       */
+  int32_t markers_per_object[4];         /* numberOfMarkersUAV1..4: split of the marker list per object  */
+  int32_t use_particle_filter;           /* bUseParticleFilter                                           */
+  uint8_t downgrade[PFMPE_MAX_MARKERS];  /* bMarkerNr1..5 -> bMarkerDowngrade                           */
+} pfmpe_launch_config;
+void pfmpe_default_launch_config(pfmpe_launch_config* cfg);
+int pfmpe_parse_launch(const char* text, pfmpe_launch_config* cfg);
+/* sensor_msgs/CameraInfo as echoed in README.md:127-143: K (9, row-major), D (plumb_bob k1 k2 p1 p2 k3),
+ * width, height (any pointer may be NULL).  Returns a bit mask of what was found (1 K, 2 D, 4 width,
+ * 8 height) or < 0 on a malformed K / D list. */
+int pfmpe_parse_camera_info(const char* text, double* K, double* D, int32_t* width, int32_t* height);
+/* Recorded detection streams (image_points_ per frame, undistorted px), little-endian binary:
+ *   header "PFMB" | u32 version = 1 | u32 n_frames | u32 reserved
+ *   frame  f64 timestamp | u32 B | u32 flags = 0 | B x {f64 x, f64 y}
+ * offsets: n_frames + 1 prefix offsets into blobs (rows), as pfmpe_stage_blob_bank.  read: call with
+ * NULL buffers to get n_frames / n_blobs; PFMPE_E_CAP if the buffers are too small. */
+int pfmpe_write_blob_stream(const char* path, const double* timestamps, const double* blobs, const int32_t* offsets,
+                            int n_frames);
+int pfmpe_read_blob_stream(const char* path, double* timestamps, double* blobs, int32_t* offsets, int max_frames,
+                           int64_t max_blobs, int* n_frames, int64_t* n_blobs);
+/* Reads a stream file and stages every frame in the context's device blob bank (bank_frame = index). */
+int pfmpe_stage_blob_stream(pfmpe_ctx* ctx, const char* path, int* n_frames);
+
 /* getPoseParticles (PE:917, which = 0: kept propagated set of the last step) and getResampledParticles
  * (PE:923, which = 1: current prior).  N x 12 doubles. */
 int pfmpe_get_particles(pfmpe_ctx* ctx, int which, double* out);

@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
     "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
+    "pfmpe_parse_marker_yaml", "pfmpe_default_launch_config", "pfmpe_parse_launch", "pfmpe_parse_camera_info",
+    "pfmpe_write_blob_stream", "pfmpe_read_blob_stream", "pfmpe_stage_blob_stream",
 )
 
 
@@ -84,6 +86,12 @@ class InitOut(C.Structure):
                 "n_candidates": self.n_candidates, "first_match": self.first_match,
                 "pairs": np.array(self.corr[: 2 * self.n_corr], dtype=np.uint32).reshape(-1, 2),
                 "predicted_pose": np.array(self.predicted_pose), "hist_total": self.hist_total}
+
+
+class LaunchConfig(C.Structure):
+    _fields_ = [("pf", Params), ("init", InitParams), ("num_objects", C.c_int32),
+                ("markers_per_object", C.c_int32 * 4), ("use_particle_filter", C.c_int32),
+                ("downgrade", C.c_uint8 * MAX_MARKERS)]
 
 
 class FrameOut(C.Structure):
@@ -149,6 +157,14 @@ def load() -> C.CDLL:
         "pfmpe_default_init_params": (None, [C.POINTER(InitParams)]),
         "pfmpe_p3p_histogram": (I, [P, dp, I, C.POINTER(C.c_uint32)]),
         "pfmpe_initialise": (I, [P, dp, I, C.POINTER(InitParams), C.POINTER(InitOut), C.POINTER(C.c_uint32)]),
+        "pfmpe_parse_marker_yaml": (I, [C.c_char_p, dp, I]),
+        "pfmpe_default_launch_config": (None, [C.POINTER(LaunchConfig)]),
+        "pfmpe_parse_launch": (I, [C.c_char_p, C.POINTER(LaunchConfig)]),
+        "pfmpe_parse_camera_info": (I, [C.c_char_p, dp, dp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+        "pfmpe_write_blob_stream": (I, [C.c_char_p, dp, dp, C.POINTER(C.c_int32), I]),
+        "pfmpe_read_blob_stream": (I, [C.c_char_p, dp, dp, C.POINTER(C.c_int32), I, I64, C.POINTER(I),
+                                       C.POINTER(I64)]),
+        "pfmpe_stage_blob_stream": (I, [P, C.c_char_p, C.POINTER(I)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -315,6 +331,12 @@ class Engine:
             self.N = int(n_particles) if n_particles else (self.N or self.max_particles)
         return d, h
 
+    def stage_blob_stream(self, path) -> int:
+        """Stage every frame of a PFMB stream file in the device blob bank; returns the frame count."""
+        n = C.c_int()
+        self._chk(self.lib.pfmpe_stage_blob_stream(self.ctx, _enc(path), C.byref(n)))
+        return n.value
+
     def get_particles(self, which: int) -> np.ndarray:
         out = np.empty((self.N, 12), dtype=np.float64)
         self._chk(self.lib.pfmpe_get_particles(self.ctx, which, _dptr(out)))
@@ -341,6 +363,75 @@ class Engine:
 
     def reset_kernel_stats(self):
         self._chk(self.lib.pfmpe_reset_kernel_stats(self.ctx))
+
+
+def _enc(x):
+    return x.encode() if isinstance(x, str) else x
+
+
+def parse_marker_yaml(text) -> np.ndarray:
+    """Marker positions (M x 3) from the reference's marker YAML (README.md:95-117)."""
+    lib = load()
+    n = lib.pfmpe_parse_marker_yaml(_enc(text), None, 0)
+    if n < 0:
+        raise PFError(n, "malformed marker YAML")
+    out = np.zeros((n, 3))
+    lib.pfmpe_parse_marker_yaml(_enc(text), _dptr(out), n)
+    return out
+
+
+def parse_launch(text) -> LaunchConfig:
+    """PF / init / marker-split parameters of a ROS launch file (pf_mpe/launch/<name>.launch)."""
+    lib = load()
+    cfg = LaunchConfig()
+    lib.pfmpe_default_launch_config(C.byref(cfg))
+    n = lib.pfmpe_parse_launch(_enc(text), C.byref(cfg))
+    if n < 0:
+        raise PFError(n, "malformed launch text")
+    cfg.n_known = n
+    return cfg
+
+
+def parse_camera_info(text) -> dict:
+    """K (3x3), D (5), width, height from a sensor_msgs/CameraInfo echo (README.md:127-143)."""
+    K = np.zeros(9)
+    D = np.zeros(5)
+    w, h = C.c_int32(), C.c_int32()
+    m = load().pfmpe_parse_camera_info(_enc(text), _dptr(K), _dptr(D), C.byref(w), C.byref(h))
+    if m < 0:
+        raise PFError(m, "malformed camera_info")
+    return {"K": K.reshape(3, 3), "D": D, "width": w.value, "height": h.value, "found": m}
+
+
+def write_blob_stream(path, frames, timestamps=None):
+    """Recorded detections (a list of B_f x 2 arrays, undistorted px) -> the PFMB stream file."""
+    offs = np.zeros(len(frames) + 1, dtype=np.int32)
+    for i, f in enumerate(frames):
+        offs[i + 1] = offs[i] + len(f)
+    allb = np.ascontiguousarray(np.concatenate([np.asarray(f, np.float64).reshape(-1, 2) for f in frames]
+                                               + [np.zeros((0, 2))]), dtype=np.float64)
+    ts = np.ascontiguousarray(np.zeros(len(frames)) if timestamps is None else timestamps, dtype=np.float64)
+    rc = load().pfmpe_write_blob_stream(_enc(path), _dptr(ts), _dptr(allb), offs.ctypes.data_as(C.POINTER(C.c_int32)),
+                                        len(frames))
+    if rc != OK:
+        raise PFError(rc, f"cannot write {path}")
+
+
+def read_blob_stream(path):
+    """PFMB stream file -> (timestamps, list of B_f x 2 arrays)."""
+    lib = load()
+    nf, nb = C.c_int(), C.c_int64()
+    rc = lib.pfmpe_read_blob_stream(_enc(path), None, None, None, 0, 0, C.byref(nf), C.byref(nb))
+    if rc != OK:
+        raise PFError(rc, f"cannot read {path}")
+    ts = np.zeros(nf.value)
+    bl = np.zeros((max(nb.value, 1), 2))
+    off = np.zeros(nf.value + 1, dtype=np.int32)
+    rc = lib.pfmpe_read_blob_stream(_enc(path), _dptr(ts), _dptr(bl), off.ctypes.data_as(C.POINTER(C.c_int32)), nf.value,
+                                    nb.value, C.byref(nf), C.byref(nb))
+    if rc != OK:
+        raise PFError(rc, f"cannot read {path}")
+    return ts, [bl[off[i]:off[i + 1]].copy() for i in range(nf.value)]
 
 
 def host_ref_uniform(seed: int, j: int, a: float, b: float) -> float:
