@@ -204,6 +204,37 @@ int pfmpe_p3p_histogram(pfmpe_ctx* ctx, const double* blobs, int B, uint32_t* hi
 int pfmpe_initialise(pfmpe_ctx* ctx, const double* blobs, int B, const pfmpe_init_params* params,
                      pfmpe_init_out* out, uint32_t* hist);
 
+/* ---------------------------------------------------------------- LED detector (§8f row 4) */
+/* LEDDetector::findLeds (pf_mpe_lib/src/led_detector.cpp:46-215) on the device for one ROI of an 8-bit
+ * grey image: threshold (THRESH_TOZERO for active markers, else THRESH_BINARY_INV), GaussianBlur (ksize
+ * from sigma, OpenCV 2.4's 8-bit integer separable path, reflect-101), findContours(RETR_EXTERNAL,
+ * CHAIN_APPROX_NONE) with 2.4's zeroed 1-pixel frame, contourArea / boundingRect / moments, the blob
+ * size-aspect-circularity filter, the centre + ROI offset (cv::Point2f) and undistortPoints(K, D, P = K).
+ * K is the context's model K.  Output: image_points_ (undistorted px, findContours order) and the
+ * distorted centres (distorted_detection_centers_).  image = NULL uses the staged image. */
+typedef struct {
+  int32_t threshold_value;          /* detection_threshold_value_ (threshold_value, README default 240) */
+  int32_t active_markers;           /* 1: THRESH_TOZERO, 0: THRESH_BINARY_INV (LD:56-59)               */
+  double gaussian_sigma;            /* gaussian_sigma_ (0.6), in (0, 5]                               */
+  double min_blob_area;             /* min_blob_area_ (the tracker's adapted value, PE:432-435)       */
+  double max_blob_area;             /* max_blob_area_                                                 */
+  double max_width_height_distortion; /* 0.7                                                          */
+  double max_circular_distortion;   /* 0.7                                                            */
+  double D[5];                      /* camera_distortion_coeffs_ k1 k2 p1 p2 k3                       */
+  int32_t roi_x, roi_y, roi_w, roi_h; /* region_of_interest_; roi_w / roi_h < 0 = the whole image   */
+} pfmpe_detect_params;
+typedef struct {
+  int32_t n;                        /* detections (all of them; min(n, max_out) written)              */
+  int32_t n_components;             /* 8-connected components (contours) examined                     */
+  int32_t overflow;                 /* more than 8192 components: the rest were not examined          */
+  int32_t pad;
+} pfmpe_detect_out;
+void pfmpe_default_detect_params(pfmpe_detect_params* p);
+int pfmpe_stage_image(pfmpe_ctx* ctx, const uint8_t* image, int width, int height, int pitch);
+int pfmpe_find_leds(pfmpe_ctx* ctx, const uint8_t* image, int width, int height, int pitch,
+                    const pfmpe_detect_params* params, double* blobs, float* distorted, int max_out,
+                    pfmpe_detect_out* out);
+
 /* ---------------------------------------- configuration files and recorded streams (§8f row 3) */
 /* Host-only (no GPU): pfmpe_io.cpp.  The reference reads these through ROS (rosparam / getParam /
  * dynamic_reconfigure, pf_mpe/src/monocular_pose_estimator.cpp:81-126, 479-527) and the CameraInfo topic.
@@ -276,7 +307,8 @@ enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduc
        PFMPE_K_FINAL = 5,     /* k_resample_final: winner + frame record (one block) */
        PFMPE_K_P3P_HIST = 6,  /* k_p3p_hist: initialisation histogram                */
        PFMPE_K_P3P_CHECK = 7, /* k_p3p_check: checkCorrespondences of all candidates */
-       PFMPE_K_COUNT = 8 };
+       PFMPE_K_DETECT = 8,    /* k_det_*: the LED detector pipeline (pfmpe_find_leds) */
+       PFMPE_K_COUNT = 9 };
 int pfmpe_get_kernel_stats(pfmpe_ctx* ctx, int kernel, int64_t* launches, double* total_ms);
 int pfmpe_reset_kernel_stats(pfmpe_ctx* ctx);
 const char* pfmpe_kernel_name(int kernel);

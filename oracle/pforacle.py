@@ -73,6 +73,13 @@ class OrcInitOut(C.Structure):
                 "predicted_pose": np.array(self.predicted_pose), "hist_total": self.hist_total}
 
 
+class OrcDetectParams(C.Structure):
+    _fields_ = [("threshold_value", C.c_int), ("gaussian_sigma", C.c_double), ("min_blob_area", C.c_double),
+                ("max_blob_area", C.c_double), ("max_width_height_distortion", C.c_double),
+                ("max_circular_distortion", C.c_double), ("active_markers", C.c_int), ("roi_x", C.c_int),
+                ("roi_y", C.c_int), ("roi_w", C.c_int), ("roi_h", C.c_int)]
+
+
 _lib = None
 
 
@@ -131,6 +138,9 @@ def load() -> C.CDLL:
     lib.orc_init_histogram_bounds.restype = C.c_int
     lib.orc_init_histogram_bounds.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.c_double, u32p, u32p, u32p,
                                               C.POINTER(C.c_int)]
+    lib.orc_find_leds.restype = C.c_int
+    lib.orc_find_leds.argtypes = [C.POINTER(C.c_uint8), C.c_int, C.c_int, C.c_int, C.POINTER(OrcDetectParams), dp, dp,
+                                  C.c_int, C.POINTER(C.c_float), dp, dp, C.POINTER(C.c_uint8)]
     lib.orc_initialise.restype = C.c_int
     lib.orc_initialise.argtypes = [C.c_int, dp, dp, C.c_int, dp, C.POINTER(OrcInitParams), C.c_int, u32p, u32p,
                                    dp, C.POINTER(OrcInitOut)]
@@ -369,3 +379,27 @@ def initialise(markers, K, blobs, n_particles, particles=None, tol=5.0, certaint
     if rc != 0:
         raise RuntimeError(f"orc_initialise failed: {rc}")
     return out.as_dict(), hout, pp
+
+
+# ------------------------------------------------------------------ LED detector (LEDDetector::findLeds)
+def find_leds(image, K, D, threshold_value=240, gaussian_sigma=0.6, min_blob_area=20, max_blob_area=160,
+              max_width_height_distortion=0.7, max_circular_distortion=0.7, active_markers=True, roi=None,
+              max_out=1024, want_mask=False):
+    """-> (undistorted B x 2, distorted B x 2 float32, areas B, mask or None)."""
+    img = np.ascontiguousarray(image, dtype=np.uint8)
+    h, w = img.shape
+    rx, ry, rw, rh = roi if roi is not None else (0, 0, w, h)
+    prm = OrcDetectParams(threshold_value, gaussian_sigma, min_blob_area, max_blob_area, max_width_height_distortion,
+                          max_circular_distortion, 1 if active_markers else 0, rx, ry, rw, rh)
+    und = np.zeros((max_out, 2))
+    dist = np.zeros((max_out, 2), dtype=np.float32)
+    areas = np.zeros(max_out)
+    mask = np.zeros((rh, rw), dtype=np.uint8) if want_mask else None
+    n = load().orc_find_leds(img.ctypes.data_as(C.POINTER(C.c_uint8)), w, h, img.strides[0], C.byref(prm),
+                             _p(_d(K).reshape(9)), _p(_d(D).reshape(5)), max_out,
+                             dist.ctypes.data_as(C.POINTER(C.c_float)), _p(und), _p(areas),
+                             mask.ctypes.data_as(C.POINTER(C.c_uint8)) if want_mask else None)
+    if n < 0:
+        raise ValueError("orc_find_leds: bad arguments")
+    n = min(n, max_out)
+    return und[:n], dist[:n], areas[:n], mask

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
-K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_COUNT = 0, 1, 2, 3, 4, 5, 6, 7, 8
+K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
 EXPORTED_SYMBOLS = (
@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
     "pfmpe_parse_marker_yaml", "pfmpe_default_launch_config", "pfmpe_parse_launch", "pfmpe_parse_camera_info",
     "pfmpe_write_blob_stream", "pfmpe_read_blob_stream", "pfmpe_stage_blob_stream",
+    "pfmpe_default_detect_params", "pfmpe_stage_image", "pfmpe_find_leds",
 )
 
 
@@ -86,6 +87,18 @@ class InitOut(C.Structure):
                 "n_candidates": self.n_candidates, "first_match": self.first_match,
                 "pairs": np.array(self.corr[: 2 * self.n_corr], dtype=np.uint32).reshape(-1, 2),
                 "predicted_pose": np.array(self.predicted_pose), "hist_total": self.hist_total}
+
+
+class DetectParams(C.Structure):
+    _fields_ = [("threshold_value", C.c_int32), ("active_markers", C.c_int32), ("gaussian_sigma", C.c_double),
+                ("min_blob_area", C.c_double), ("max_blob_area", C.c_double),
+                ("max_width_height_distortion", C.c_double), ("max_circular_distortion", C.c_double),
+                ("D", C.c_double * 5), ("roi_x", C.c_int32), ("roi_y", C.c_int32), ("roi_w", C.c_int32),
+                ("roi_h", C.c_int32)]
+
+
+class DetectOut(C.Structure):
+    _fields_ = [("n", C.c_int32), ("n_components", C.c_int32), ("overflow", C.c_int32), ("pad", C.c_int32)]
 
 
 class LaunchConfig(C.Structure):
@@ -165,6 +178,10 @@ def load() -> C.CDLL:
         "pfmpe_read_blob_stream": (I, [C.c_char_p, dp, dp, C.POINTER(C.c_int32), I, I64, C.POINTER(I),
                                        C.POINTER(I64)]),
         "pfmpe_stage_blob_stream": (I, [P, C.c_char_p, C.POINTER(I)]),
+        "pfmpe_default_detect_params": (None, [C.POINTER(DetectParams)]),
+        "pfmpe_stage_image": (I, [P, C.POINTER(C.c_uint8), I, I, I]),
+        "pfmpe_find_leds": (I, [P, C.POINTER(C.c_uint8), I, I, I, C.POINTER(DetectParams), dp,
+                                C.POINTER(C.c_float), I, C.POINTER(DetectOut)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -330,6 +347,38 @@ class Engine:
         if d["found"]:
             self.N = int(n_particles) if n_particles else (self.N or self.max_particles)
         return d, h
+
+    def stage_image(self, image: np.ndarray):
+        img = np.ascontiguousarray(image, dtype=np.uint8)
+        self._chk(self.lib.pfmpe_stage_image(self.ctx, img.ctypes.data_as(C.POINTER(C.c_uint8)), img.shape[1],
+                                             img.shape[0], img.strides[0]))
+        self._img_shape = img.shape
+
+    def find_leds(self, image=None, D=None, roi=None, max_out=MAX_BLOBS, **kw):
+        """LEDDetector::findLeds (led_detector.cpp:46-215) on the device -> (undistorted B x 2,
+        distorted B x 2 float32, info).  image None: the staged image.  kw: DetectParams fields."""
+        p = DetectParams()
+        self.lib.pfmpe_default_detect_params(C.byref(p))
+        if D is not None:
+            p.D[:] = list(np.asarray(D, np.float64).reshape(5))
+        if roi is not None:
+            p.roi_x, p.roi_y, p.roi_w, p.roi_h = [int(v) for v in roi]
+        for k, v in kw.items():
+            setattr(p, k, v)
+        blobs = np.zeros((max(max_out, 1), 2))
+        dist = np.zeros((max(max_out, 1), 2), dtype=np.float32)
+        out = DetectOut()
+        if image is not None:
+            img = np.ascontiguousarray(image, dtype=np.uint8)
+            ip, (h, w), pitch = img.ctypes.data_as(C.POINTER(C.c_uint8)), img.shape, img.strides[0]
+        else:
+            ip, (h, w) = C.POINTER(C.c_uint8)(), self._img_shape
+            pitch = w
+        self._chk(self.lib.pfmpe_find_leds(self.ctx, ip, w, h, pitch, C.byref(p), _dptr(blobs),
+                                           dist.ctypes.data_as(C.POINTER(C.c_float)), max_out, C.byref(out)))
+        n = min(out.n, max_out)
+        return blobs[:n].copy(), dist[:n].copy(), {"n": out.n, "n_components": out.n_components,
+                                                    "overflow": out.overflow}
 
     def stage_blob_stream(self, path) -> int:
         """Stage every frame of a PFMB stream file in the device blob bank; returns the frame count."""

@@ -61,6 +61,11 @@ struct pfmpe_ctx {
   double* d_roi = nullptr;         // ROI box [4] + per-block partials
   unsigned char* d_init = nullptr; // initialisation scratch (pfmpe_init.hip), grown on demand
   size_t init_cap = 0;
+  unsigned char* d_det = nullptr;  // detector scratch (pfmpe_detect.hip), grown on demand
+  size_t det_cap = 0;
+  uint8_t* d_img = nullptr;        // staged camera image (pfmpe_stage_image)
+  size_t img_cap = 0;
+  int img_w = 0, img_h = 0, img_pitch = 0;
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
   bool fused = true;               // PFMPE_OPT_FUSED

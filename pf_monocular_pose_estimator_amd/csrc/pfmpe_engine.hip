@@ -81,7 +81,7 @@ void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* 
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
-                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_roi, c->d_init, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -580,7 +580,8 @@ int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
 
 const char* pfmpe_kernel_name(int kernel) {
   static const char* names[PFMPE_K_COUNT] = {"k_propagate_weigh", "k_resample", "aux", "k_frame", "k_roi",
-                                                 "k_resample_final", "k_p3p_hist", "k_p3p_check"};
+                                                 "k_resample_final", "k_p3p_hist", "k_p3p_check",
+                                                 "k_det (detector pipeline)"};
   return (kernel >= 0 && kernel < PFMPE_K_COUNT) ? names[kernel] : "?";
 }
 

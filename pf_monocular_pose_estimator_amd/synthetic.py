@@ -275,3 +275,38 @@ def init_blobs(M: int = 5, n_out: int = 3, seed: int = 0, noise_px: float = 0.0,
     blobs = np.array(blobs)
     rng.shuffle(blobs)
     return blobs.astype(np.float32).astype(np.float64), T
+
+
+def distort_px(K, D, uv: np.ndarray) -> np.ndarray:
+    """plumb_bob distortion of ideal pixel positions (what the camera sees)."""
+    k1, k2, p1, p2, k3 = D
+    x = (uv[:, 0] - K[0, 2]) / K[0, 0]
+    y = (uv[:, 1] - K[1, 2]) / K[1, 1]
+    r2 = x * x + y * y
+    rad = 1 + k1 * r2 + k2 * r2 * r2 + k3 * r2 ** 3
+    xd = x * rad + 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+    yd = y * rad + p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+    return np.stack([xd * K[0, 0] + K[0, 2], yd * K[1, 1] + K[1, 2]], axis=1)
+
+
+def led_image(T: np.ndarray, markers: np.ndarray, seed: int = 0, radius: float = 3.2, n_false: int = 3,
+              W: int = IMAGE_W, H: int = IMAGE_H, noise: int = 60):
+    """An 8-bit camera image of the LED object at pose T (LEDDetector::findLeds input, led_detector.cpp:46):
+    saturated discs (radius px, soft 1-px edge) at the DISTORTED projections of the markers, `n_false`
+    bright distractors (discs and an elongated bar), uniform background noise.  Returns (image H x W
+    uint8, ideal undistorted projections M x 2)."""
+    rng = np.random.default_rng(9000 + seed)
+    img = rng.integers(0, noise + 1, size=(H, W)).astype(np.float64)
+    ideal = project(K_README, T, markers)
+    centres = list(distort_px(K_README, D_README, ideal))
+    for _ in range(n_false):
+        centres.append(np.array([rng.uniform(20, W - 20), rng.uniform(20, H - 20)]))
+    yy, xx = np.mgrid[0:H, 0:W]
+    for i, (cx, cy) in enumerate(centres):
+        d = np.hypot(xx - cx, yy - cy)
+        spot = np.clip(radius + 1.0 - d, 0.0, 1.0) * 255.0
+        img = np.maximum(img, spot)
+    if n_false:
+        x0, y0 = int(rng.uniform(40, W - 80)), int(rng.uniform(40, H - 40))
+        img[y0:y0 + 3, x0:x0 + 30] = 255.0  # elongated: fails the aspect filter
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8), ideal
