@@ -66,6 +66,7 @@ struct pfmpe_ctx {
   uint8_t* d_img = nullptr;        // staged camera image (pfmpe_stage_image)
   size_t img_cap = 0;
   int img_w = 0, img_h = 0, img_pitch = 0;
+  void* h_det = nullptr;           // detector output record (pinned, host-mapped)
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
   bool fused = true;               // PFMPE_OPT_FUSED

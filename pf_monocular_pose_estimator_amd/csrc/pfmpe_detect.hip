@@ -6,13 +6,15 @@
 //                  reflect-101 borders, (sum + 2^15) >> 16) -> "pixel is nonzero" mask, with the 1-pixel
 //                  frame cvStartFindContours zeroes.  16x16 tiles: thresholded tile + halo, then the row
 //                  pass, staged in LDS; exact integer arithmetic.
-//   k_det_label    per foreground pixel: its 8-neighbour bit mask (bit s = direction s of icvFetchContour's
-//                  table) and its own index as label
-//   k_det_merge    union-find over the 8-connectivity (W, NW, N, NE), atomicMin links to the lower index
-//                  (agent-scope loads in find: other blocks' links bypass the non-coherent L1)
+//   k_det_label    per 32x32 tile in LDS: each pixel's 8-neighbour bit mask (bit s = direction s of
+//                  icvFetchContour's table) and a tile-local union-find (W, NW, N, NE; atomicMin links to the
+//                  lower index); the label is the local root's image index
+//   k_det_merge    the global union-find over the links that cross tile borders only (agent-scope loads
+//                  in find: other blocks' links bypass the non-coherent L1)
 //   k_det_roots    flatten; every root (= the component's raster-first pixel, where the reference's raster
 //                  scan starts its outer border) takes a slot
-//   k_det_trace    one lane per component: icvFetchContour's border following over the neighbour masks,
+//   k_det_trace    one wave per component (grid-stride over the slots): a 64x64 window of neighbour masks
+//                  staged in LDS, then lane 0 runs icvFetchContour's border following over it,
 //                  polygon moments / area / bounding box on the fly, the size-aspect-circularity filter,
 //                  the centre + ROI offset as float, cvUndistortPoints (5 iterations, P = K)
 // The host orders the accepted detections as findContours returns them (reverse discovery = descending
@@ -86,26 +88,88 @@ __global__ __launch_bounds__(kDetTile* kDetTile) void k_det_mask(const DetArgs a
   mask[(int64_t)y * a.W + x] = (v > 0 && !frame) ? 1 : 0;
 }
 
-// neighbour bits: bit s = the pixel in direction s is foreground (0 +x, 1 (+x,-y), 2 -y, 3 (-x,-y),
-// 4 -x, 5 (-x,+y), 6 +y, 7 (+x,+y))
-__global__ void k_det_label(const DetArgs a, const uint8_t* __restrict__ mask, uint8_t* __restrict__ nbr,
-                            int* __restrict__ label) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)a.W * a.H) return;
-  const int y = (int)(i / a.W), x = (int)(i - (int64_t)y * a.W);
-  if (!mask[i]) {
-    label[i] = -1;
-    nbr[i] = 0;
-    return;
-  }
-  uint32_t bits = 0;
+// Labelling, tile-local first: a 32 x 32 tile (+1 halo) of the mask in LDS gives each pixel its 8-neighbour
+// bit mask (bit s = direction s of icvFetchContour's table: 0 +x, 1 (+x,-y), 2 -y, 3 (-x,-y), 4 -x,
+// 5 (-x,+y), 6 +y, 7 (+x,+y)) and an LDS union-find over the tile's own W / NW / N / NE links (atomicMin
+// to the lower index: the local root is the component's raster-first pixel in the tile).  The global
+// label is that root's image index; k_det_merge then unites only links that cross a tile border.
+constexpr int kLT = 32;
+__device__ __forceinline__ int lfind(const int* L, int i) {
+  for (int p = L[i]; p != i; p = L[i]) i = p;
+  return i;
+}
+constexpr int kLabelBlock = 1024;
+__global__ __launch_bounds__(kLabelBlock) void k_det_label(const DetArgs a, const uint8_t* __restrict__ mask,
+                                                   uint8_t* __restrict__ nbr, int* __restrict__ label) {
+  __shared__ uint8_t m[kLT + 2][kLT + 2];
+  __shared__ int L[kLT * kLT];
+  const int x0 = blockIdx.x * kLT, y0 = blockIdx.y * kLT;
+  {  // branch-free: clamped in-bounds addresses, all loads in flight, then the selects
+    constexpr int kN = ((kLT + 2) * (kLT + 2) + kLabelBlock - 1) / kLabelBlock;
+    uint32_t v[kN];
+    bool in[kN];
 #pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    const int nx = x + dir_dx(s), ny = y + dir_dy(s);
-    if (nx >= 0 && ny >= 0 && nx < a.W && ny < a.H && mask[(int64_t)ny * a.W + nx]) bits |= 1u << s;
+    for (int q = 0; q < kN; ++q) {
+      const int i = threadIdx.x + kLabelBlock * q;
+      const int ty = i / (kLT + 2), tx = i - ty * (kLT + 2);
+      const int gx = x0 + tx - 1, gy = y0 + ty - 1;
+      in[q] = i < (kLT + 2) * (kLT + 2) && gx >= 0 && gy >= 0 && gx < a.W && gy < a.H;
+      v[q] = mask[(int64_t)min(max(gy, 0), a.H - 1) * a.W + min(max(gx, 0), a.W - 1)];
+    }
+#pragma unroll
+    for (int q = 0; q < kN; ++q) {
+      const int i = threadIdx.x + kLabelBlock * q;
+      if (i < (kLT + 2) * (kLT + 2)) m[i / (kLT + 2)][i % (kLT + 2)] = in[q] ? (uint8_t)v[q] : (uint8_t)0;
+    }
   }
-  nbr[i] = (uint8_t)bits;
-  label[i] = (int)i;
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLT * kLT; i += blockDim.x) {
+    const int ly = i / kLT, lx = i - ly * kLT;
+    L[i] = m[ly + 1][lx + 1] ? i : -1;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLT * kLT; i += blockDim.x) {
+    const int ly = i / kLT, lx = i - ly * kLT;
+    if (!m[ly + 1][lx + 1]) continue;
+    const int nb[4][2] = {{-1, 0}, {-1, -1}, {0, -1}, {1, -1}};  // W, NW, N, NE
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nx = lx + nb[q][0], ny = ly + nb[q][1];
+      if (nx < 0 || ny < 0 || nx >= kLT || !m[ny + 1][nx + 1]) continue;
+      int u = i, v = ny * kLT + nx;
+      for (;;) {  // LDS union-find: link the higher root to the lower index
+        u = lfind(L, u);
+        v = lfind(L, v);
+        if (u == v) break;
+        if (u < v) {
+          const int t = u;
+          u = v;
+          v = t;
+        }
+        const int old = atomicMin(&L[u], v);
+        if (old == u) break;
+        u = old;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < kLT * kLT; i += blockDim.x) {
+    const int ly = i / kLT, lx = i - ly * kLT;
+    const int gx = x0 + lx, gy = y0 + ly;
+    if (gx >= a.W || gy >= a.H) continue;
+    const int64_t g = (int64_t)gy * a.W + gx;
+    if (!m[ly + 1][lx + 1]) {
+      label[g] = -1;
+      nbr[g] = 0;
+      continue;
+    }
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) bits |= m[ly + 1 + dir_dy(s)][lx + 1 + dir_dx(s)] ? 1u << s : 0u;
+    nbr[g] = (uint8_t)bits;
+    const int r = lfind(L, i);
+    label[g] = (y0 + r / kLT) * a.W + (x0 + r % kLT);
+  }
 }
 
 __device__ __forceinline__ int ld_label(const int* L, int i) {
@@ -131,16 +195,20 @@ __device__ __forceinline__ void unite(int* L, int a, int b) {
   }
 }
 
+// the links that cross a tile border (the left column's W / NW, the top row's NW / N / NE)
 __global__ void k_det_merge(const DetArgs a, const uint8_t* __restrict__ nbr, int* __restrict__ label) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)a.W * a.H) return;
+  const int W = a.W;
+  const int y = (int)(i / W), x = (int)(i - (int64_t)y * W);
+  const bool left = (x % kLT) == 0, top = (y % kLT) == 0, right = (x % kLT) == kLT - 1;
+  if (!left && !top && !right) return;
   const uint32_t b = nbr[i];
   if (!b) return;
-  const int W = a.W;
-  if (b & (1u << 4)) unite(label, (int)i, (int)i - 1);
-  if (b & (1u << 3)) unite(label, (int)i, (int)i - W - 1);
-  if (b & (1u << 2)) unite(label, (int)i, (int)i - W);
-  if (b & (1u << 1)) unite(label, (int)i, (int)i - W + 1);
+  if (left && (b & (1u << 4))) unite(label, (int)i, (int)i - 1);
+  if ((left || top) && (b & (1u << 3))) unite(label, (int)i, (int)i - W - 1);
+  if (top && (b & (1u << 2))) unite(label, (int)i, (int)i - W);
+  if ((top || right) && (b & (1u << 1))) unite(label, (int)i, (int)i - W + 1);
 }
 
 __global__ void k_det_roots(const DetArgs a, const uint8_t* __restrict__ mask, int* __restrict__ label,
@@ -156,26 +224,55 @@ __global__ void k_det_roots(const DetArgs a, const uint8_t* __restrict__ mask, i
   }
 }
 
-__global__ void k_det_trace(const DetArgs a, const uint8_t* __restrict__ nbr, const int* __restrict__ count,
-                            const int* __restrict__ roots, DetRecord* __restrict__ rec) {
-  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+// One block (one wave) per component slot: the wave stages a 64 x 64 window of neighbour masks (rows
+// y0 .. y0+63 from the root down, columns x0-31 .. x0+32) in LDS, then lane 0 follows the border there
+// (a point outside the window falls back to the global masks).
+constexpr int kWin = 64;
+__global__ __launch_bounds__(64) void k_det_trace(const DetArgs a, const uint8_t* __restrict__ nbr,
+                                                  const int* __restrict__ count, const int* __restrict__ roots,
+                                                  DetRecord* __restrict__ rec) {
+  __shared__ uint8_t win[kWin][kWin];
   const int nc = min(*count, kDetMaxComponents);
-  if (slot >= nc) return;
+  for (int slot = blockIdx.x; slot < nc; slot += gridDim.x) {
+  __syncthreads();  // the previous slot's window reads are done
   const int root = roots[slot];
   const int W = a.W;
   const int x0 = root % W, y0 = root / W;
+  const int wx = x0 - kWin / 2 + 1, wy = y0;
+  {  // branch-free: every lane loads from a clamped in-bounds address, 16 loads in flight per batch
+    const int lane = threadIdx.x;
+    const int gx = wx + lane;
+    const bool xin = gx >= 0 && gx < W;
+    const int cx = min(max(gx, 0), W - 1);
+    for (int r0 = 0; r0 < kWin; r0 += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = nbr[(int64_t)min(wy + r0 + q, a.H - 1) * W + cx];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) win[r0 + q][lane] = (xin && wy + r0 + q < a.H) ? (uint8_t)v[q] : (uint8_t)0;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+  auto nb = [&](int x, int y) -> uint32_t {
+    const int lx = x - wx, ly = y - wy;
+    if ((unsigned)lx < (unsigned)kWin && (unsigned)ly < (unsigned)kWin) return win[ly][lx];
+    return nbr[(int64_t)y * W + x];
+  };
   // icvFetchContour (CHAIN_APPROX_NONE), the contour points streamed into the polygon sums
-  double a00 = 0, a10 = 0, a01 = 0, area2 = 0;
+  // The reference sums these in double; every term is an integer far below 2^53, so int64 sums are the
+  // same numbers (exact either way) with a shorter dependency chain.
+  int64_t a00 = 0, a10 = 0, a01 = 0, area2 = 0;
   int minx = x0, maxx = x0, miny = y0, maxy = y0;
-  double fx_ = 0, fy_ = 0, px_ = 0, py_ = 0;  // first point, previous point
+  int64_t fx_ = 0, fy_ = 0, px_ = 0, py_ = 0;  // first point, previous point
   int np = 0;
   auto add_point = [&](int x, int y) {
-    const double xi = x, yi = y;
+    const int64_t xi = x, yi = y;
     if (np == 0) {
       fx_ = xi;
       fy_ = yi;
     } else {
-      const double dxy = px_ * yi - xi * py_;
+      const int64_t dxy = px_ * yi - xi * py_;
       a00 += dxy;
       a10 += dxy * (px_ + xi);
       a01 += dxy * (py_ + yi);
@@ -189,20 +286,20 @@ __global__ void k_det_trace(const DetArgs a, const uint8_t* __restrict__ nbr, co
     maxy = max(maxy, y);
     ++np;
   };
-  const uint32_t b0 = nbr[root];
+  const uint32_t b0 = nb(x0, y0);
   int s = 4;
   do {
     s = (s - 1) & 7;
   } while (!((b0 >> s) & 1u) && s != 4);
-  if (s == 4 && !((b0 >> 4) & 1u)) {
+  if (s == 4) {
     add_point(x0, y0);  // single-pixel domain
   } else {
     const int x1 = x0 + dir_dx(s), y1 = y0 + dir_dy(s);
     int x3 = x0, y3 = y0, px = x0, py = y0;
-    for (int guard = 0; guard < 4 * a.W * a.H + 8; ++guard) {
-      const uint32_t bb = nbr[(int64_t)y3 * W + x3];
+    for (int64_t guard = 0; guard < 4 * (int64_t)a.W * a.H + 8; ++guard) {
+      const uint32_t bb = nb(x3, y3);
       const uint32_t rot = ((bb | (bb << 8)) >> ((s + 1) & 7)) & 0xffu;  // directions s+1, s+2, ... (cyclic)
-      s = (s + 1 + __builtin_ctz(rot)) & 7;                            // first set (>= 1 exists)
+      s = (s + 1 + __builtin_ctz(rot)) & 7;                            // first set (one exists)
       const int x4 = x3 + dir_dx(s), y4 = y3 + dir_dy(s);
       add_point(px, py);
       px += dir_dx(s);
@@ -216,21 +313,21 @@ __global__ void k_det_trace(const DetArgs a, const uint8_t* __restrict__ nbr, co
   // closing edge last -> first (the reference's loop starts from the last point; the sums are the
   // same terms in a rotated order: exact for these integer-valued products)
   if (np > 1) {
-    const double xi = fx_, yi = fy_;
-    const double dxy = px_ * yi - xi * py_;
+    const int64_t xi = fx_, yi = fy_;
+    const int64_t dxy = px_ * yi - xi * py_;
     a00 += dxy;
     a10 += dxy * (px_ + xi);
     a01 += dxy * (py_ + yi);
     area2 += px_ * yi - py_ * xi;
   }
   double m00 = 0, m10 = 0, m01 = 0;
-  if (fabs(a00) > 1.1920928955078125e-07) {
+  if (a00 != 0) {  // |a00| > FLT_EPSILON for an integer
     const double s2 = a00 > 0 ? 0.5 : -0.5, s6 = a00 > 0 ? 1.0 / 6 : -1.0 / 6;
-    m00 = a00 * s2;
-    m10 = a10 * s6;
-    m01 = a01 * s6;
+    m00 = (double)a00 * s2;
+    m10 = (double)a10 * s6;
+    m01 = (double)a01 * s6;
   }
-  const double area = fabs(area2 * 0.5);
+  const double area = fabs((double)area2 * 0.5);
   const int rw = maxx - minx + 1, rh = maxy - miny + 1;
   const double pi = 3.1415926535897932384626433832795;
   const double hw = (double)(rw / 2), hh = (double)(rh / 2);  // the reference's integer rect.width / 2
@@ -266,6 +363,46 @@ __global__ void k_det_trace(const DetArgs a, const uint8_t* __restrict__ nbr, co
     o.uy = (double)(float)(yy * ww);
   }
   rec[slot] = o;
+  }  // lane 0
+  }  // slots
+}
+
+// Output in findContours order (reverse discovery = descending root index), written straight into pinned
+// host memory: rank of a kept record = number of kept records with a larger root.  One block.
+struct DetOutHost {
+  int32_t n, n_components, overflow, pad;
+  double und[2 * kMaxBlobs];
+  float dist[2 * kMaxBlobs];
+};
+constexpr int kEmitBlock = 1024;
+__global__ __launch_bounds__(kEmitBlock) void k_det_emit(const int* __restrict__ count, const DetRecord* __restrict__ rec,
+                                                         DetOutHost* __restrict__ out) {
+  __shared__ int kroot[kDetMaxComponents];
+  __shared__ int nkept;
+  const int nc = min(*count, kDetMaxComponents);
+  if (threadIdx.x == 0) nkept = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nc; i += kEmitBlock)
+    if (rec[i].keep) kroot[atomicAdd(&nkept, 1)] = i;  // slot ids, any order
+  __syncthreads();
+  const int nk = nkept;
+  for (int t = threadIdx.x; t < nk; t += kEmitBlock) {
+    const int i = kroot[t];
+    const int r = rec[i].root;
+    int rank = 0;
+    for (int u = 0; u < nk; ++u) rank += rec[kroot[u]].root > r ? 1 : 0;
+    if (rank < kMaxBlobs) {
+      out->und[2 * rank] = rec[i].ux;
+      out->und[2 * rank + 1] = rec[i].uy;
+      out->dist[2 * rank] = rec[i].dx;
+      out->dist[2 * rank + 1] = rec[i].dy;
+    }
+  }
+  if (threadIdx.x == 0) {
+    out->n = nk;
+    out->n_components = *count;
+    out->overflow = *count > kDetMaxComponents ? 1 : 0;
+  }
 }
 
 }  // namespace pfmpe
@@ -407,44 +544,35 @@ int pfmpe_find_leds(pfmpe_ctx* c, const uint8_t* image, int width, int height, i
   HIPCHK(c, hipMemsetAsync(b.count, 0, sizeof(int), c->stream));
   const unsigned g1 = (unsigned)((npix + 255) / 256);
   c->timing_now = c->timing > 0;
+  if (!c->h_det) {
+    HIPCHK(c, hipHostMalloc((void**)&c->h_det, sizeof(DetOutHost), hipHostMallocMapped | hipHostMallocCoherent));
+  }
+  DetOutHost* hout = (DetOutHost*)c->h_det;
+  DetOutHost* dout = nullptr;
+  HIPCHK(c, hipHostGetDevicePointer((void**)&dout, hout, 0));
   RET(launch(c, PFMPE_K_DETECT, [&] {
     hipLaunchKernelGGL(k_det_mask, dim3((W + kDetTile - 1) / kDetTile, (H + kDetTile - 1) / kDetTile),
                        dim3(kDetTile * kDetTile), 0, c->stream, a, c->d_img, b.mask);
-    hipLaunchKernelGGL(k_det_label, dim3(g1), dim3(256), 0, c->stream, a, b.mask, b.nbr, b.label);
+    hipLaunchKernelGGL(k_det_label, dim3((W + kLT - 1) / kLT, (H + kLT - 1) / kLT), dim3(kLabelBlock), 0, c->stream, a, b.mask,
+                       b.nbr, b.label);
     hipLaunchKernelGGL(k_det_merge, dim3(g1), dim3(256), 0, c->stream, a, b.nbr, b.label);
     hipLaunchKernelGGL(k_det_roots, dim3(g1), dim3(256), 0, c->stream, a, b.mask, b.label, b.count, b.roots);
-    hipLaunchKernelGGL(k_det_trace, dim3(kDetMaxComponents / 64), dim3(64), 0, c->stream, a, b.nbr, b.count, b.roots,
-                       b.rec);
+    hipLaunchKernelGGL(k_det_trace, dim3(512), dim3(64), 0, c->stream, a, b.nbr, b.count, b.roots, b.rec);
+    hipLaunchKernelGGL(k_det_emit, dim3(1), dim3(kEmitBlock), 0, c->stream, b.count, b.rec, dout);
   }));
-  int nc = 0;
-  HIPCHK(c, hipMemcpyAsync(&nc, b.count, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  const int ncs = std::min(nc, kDetMaxComponents);
-  std::vector<DetRecord> rec(ncs);
-  if (ncs > 0) {
-    HIPCHK(c, hipMemcpyAsync(rec.data(), b.rec, ncs * sizeof(DetRecord), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-  }
   if (c->timing_now) RET(harvest_timing(c));
   c->timing_now = false;
-  // findContours order: reverse discovery = descending raster index of the start pixel
-  std::sort(rec.begin(), rec.end(), [](const DetRecord& x, const DetRecord& y) { return x.root > y.root; });
-  int m = 0;
-  for (const DetRecord& r : rec) {
-    if (!r.keep) continue;
-    if (m < max_out) {
-      blobs[2 * m] = r.ux;
-      blobs[2 * m + 1] = r.uy;
-      if (distorted) {
-        distorted[2 * m] = r.dx;
-        distorted[2 * m + 1] = r.dy;
-      }
-    }
-    ++m;
+  const int m = hout->n;
+  const int nc = hout->n_components;
+  const int nw = std::min(std::min(m, max_out), kMaxBlobs);
+  if (nw > 0) {
+    std::memcpy(blobs, hout->und, 2 * (size_t)nw * sizeof(double));
+    if (distorted) std::memcpy(distorted, hout->dist, 2 * (size_t)nw * sizeof(float));
   }
   out->n = m;
   out->n_components = nc;
-  out->overflow = nc > kDetMaxComponents ? 1 : 0;
+  out->overflow = hout->overflow;
   return PFMPE_OK;
 }
 

@@ -87,6 +87,7 @@ void free_all(pfmpe_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->h_out) (void)hipHostFree(c->h_out);
   if (c->h_table) (void)hipHostFree(c->h_table);
+  if (c->h_det) (void)hipHostFree(c->h_det);
   for (auto& e : c->ev_pool) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);

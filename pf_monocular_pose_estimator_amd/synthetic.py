@@ -299,14 +299,19 @@ def led_image(T: np.ndarray, markers: np.ndarray, seed: int = 0, radius: float =
     img = rng.integers(0, noise + 1, size=(H, W)).astype(np.float64)
     ideal = project(K_README, T, markers)
     centres = list(distort_px(K_README, D_README, ideal))
-    for _ in range(n_false):
-        centres.append(np.array([rng.uniform(20, W - 20), rng.uniform(20, H - 20)]))
+    while len(centres) < len(ideal) + n_false:  # distractors >= 20 px from every LED (no merged blobs)
+        c = np.array([rng.uniform(20, W - 20), rng.uniform(20, H - 20)])
+        if min(np.hypot(*(c - q)) for q in centres) >= 20:
+            centres.append(c)
     yy, xx = np.mgrid[0:H, 0:W]
     for i, (cx, cy) in enumerate(centres):
         d = np.hypot(xx - cx, yy - cy)
         spot = np.clip(radius + 1.0 - d, 0.0, 1.0) * 255.0
         img = np.maximum(img, spot)
     if n_false:
-        x0, y0 = int(rng.uniform(40, W - 80)), int(rng.uniform(40, H - 40))
+        for _ in range(100):
+            x0, y0 = int(rng.uniform(40, W - 80)), int(rng.uniform(40, H - 40))
+            if min(np.hypot(*(np.array([x0 + 15, y0 + 1]) - q)) for q in centres) >= 35:
+                break
         img[y0:y0 + 3, x0:x0 + 30] = 255.0  # elongated: fails the aspect filter
     return np.clip(np.rint(img), 0, 255).astype(np.uint8), ideal
