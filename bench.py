@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
                     "workload; default profiles/pmc_<config>_n<N>.json when present")
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
+    ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
+                    help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
     return ap.parse_args()
 
 
@@ -62,6 +64,7 @@ def algorithmic_bytes(S: int, N: int) -> dict:
         "k_propagate_weigh": N * (S + 4),      # read prior state, write weight
         "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
         "k_frame": N * (S + 4 + S),             # one launch: read prior, write weight, write new prior
+        "k_frame2": N * (S + 4 + S),
         "k_resample_final": 8 * -(-N // 256),   # read the block count partials
         "aux": 0,
     }
@@ -140,6 +143,7 @@ def main():
     prm.rng_mode = pf.RNG_PHILOX if args.rng == "philox" else pf.RNG_REFERENCE
     eng.set_params(prm)
     eng.set_prior(st.prior())
+    eng.set_option(pf.OPT_FUSED, args.fused)
     if args.diag:
         eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])

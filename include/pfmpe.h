@@ -285,9 +285,10 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *   PFMPE_OPT_PRUNE         [1|0]  exact x-window blob pruning in the likelihood (0 = scan all B blobs)
  *   PFMPE_OPT_TIMING        [0|P]  bracket the kernel launches of every P-th frame with HIP events
  *                                  (pfmpe_get_kernel_stats); P = 1 times every frame, 0 is off
- *   PFMPE_OPT_FUSED         [1|0]  run a frame as ONE cooperative launch (k_frame) whenever all its
- *                                  blocks fit on the device at once (default 1); 0 forces the
- *                                  two-launch path (k_propagate_weigh + k_resample) */
+ *   PFMPE_OPT_FUSED         [2|1|0] run a frame as ONE launch whenever all its blocks fit on the device
+ *                                  at once: 2 (default) k_frame2 with flat hand-offs (every block reduces
+ *                                  all block partials itself; <= 512 blocks), 1 k_frame with tree
+ *                                  hand-offs; 0 forces the two-launch path (k_propagate_weigh + k_resample) */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 

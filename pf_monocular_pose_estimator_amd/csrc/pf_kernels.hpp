@@ -73,6 +73,7 @@ struct FrameArgsT {
   int32_t cam_identity, max_iter, force_iters, nblk;
   int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
   int32_t diag, pad_;             // diagnostic switches (0 in production)
+  uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
   int64_t ld;                     // SoA plane stride in elements
   T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
 };
@@ -810,6 +811,39 @@ __device__ __forceinline__ void stamp_max(uint64_t* st, int idx, uint64_t t) {
   if (st) st[(size_t)(1 + blockIdx.x) * kStamps + idx] = t;
 }
 
+// ---- flat hand-off (k_frame2): sharded, monotonic arrival counters (no resets: the host tracks the running
+// totals and passes this frame's bases, uint32 arithmetic that wraps consistently).  A counter set is
+// kShards counters one 128-B line apart; an arrival goes to shard blk % kShards (one XCD's blocks under
+// round-robin placement: speed only).  Set 0: weighing barrier (one arrival per block per iteration),
+// set 1: count barrier (one per block per resampled frame).
+constexpr int kShards = 8;
+constexpr int kShardStride = 32;                         // uint32 words: 128 B
+constexpr int kFlatCountSet = kShards * kShardStride;    // offset of set 1
+constexpr int kFlatWords = 2 * kShards * kShardStride;
+constexpr int kFlatMaxGroups = 8;                        // k_frame2: <= 512 blocks in groups of 64
+__device__ __forceinline__ void flat_arrive(uint32_t* set, int blk) {  // one lane, after its sc1 stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_fetch_add((gu32_t*)(set + (blk & (kShards - 1)) * kShardStride), 1u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+// one wave: poll the set until its shards sum to `target` (true), or give up after ~2 s (false)
+__device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target) {
+  const int lane = lane_id();
+  const uint64_t t0 = rt_now();
+  for (;;) {
+    uint32_t v = 0;
+    if (lane < kShards)
+      v = __hip_atomic_load((gu32_t*)(set + lane * kShardStride), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kShards; ++k) sum += (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+    if (sum == target) return true;
+    if (rt_now() - t0 > 200000000ull) return false;  // 2 s at 100 MHz
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+
 // ============================================================================== kernels
 // ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into bucket_count(B) x-buckets,
 // built once per frame on the host (build_blob_table_host, O(B)) and copied whole into each block's
@@ -1151,16 +1185,20 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
 // ---- one particle through the motion model, projection and likelihood (PE:543-604, PE:2385)
 template <typename T, int RNG, int MAXM, bool PRUNE>
 __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
-                                            const T* A, int n, int iter, T* P, int* nvisit = nullptr) {
+                                            const T* A, int n, int iter, T* P, int* nvisit = nullptr,
+                                            uint64_t* st = nullptr) {
   T u[MAXM], v[MAXM];
   propagate<T, RNG>(fa, sc, A, n, iter, P);
+  if (st && threadIdx.x == 0) stamp_max(st, 27, rt_now() + (P[11] == (T)12345 ? 1 : 0));
   project_markers<T, MAXM>(fa, sc, P, u, v);
+  if (st && threadIdx.x == 0) stamp_max(st, 28, rt_now() + (u[0] == (T)12345 ? 1 : 0));
   T w = (T)0;
   if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
     T m[MAXM];
     int r[MAXM];
     const int visited = column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
     if (nvisit) *nvisit = visited;
+    if (st && threadIdx.x == 0) stamp_max(st, 29, rt_now() + (m[0] == (T)12345 ? 1 : 0));
     w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
   }
   return w;
@@ -1501,9 +1539,11 @@ struct ResampleLds {
 // ---- stratified resampling of one block (PE:666-682) + count partials -> winner -> frame record.
 // wd: the thread's kept raw weight (0 for invalid lanes); P: its kept propagated particle when have_P,
 // else regenerated here from A (P_in unused).  Called by every thread; the caller checked c.done && c.accepted.
-// INLAUNCH (k_frame): the block also publishes its winner candidate and the last arriver finishes the
-// frame.  Otherwise (k_resample) the block only stores its count partial; k_resample_final finishes.
-template <typename T, int RNG, int MAXM, typename SP, bool INLAUNCH>
+// MODE 1 (k_frame): the block also publishes its winner candidate and the last arriver of the count tree
+// finishes the frame.  MODE 2 (k_frame2): the same candidate, then a flat arrival on the sharded count
+// counters; block 0 waits for all of them and finishes.  MODE 0 (k_resample) the block only stores its
+// count partial; k_resample_final finishes.
+template <typename T, int RNG, int MAXM, typename SP, int MODE>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
@@ -1511,7 +1551,8 @@ __device__ __forceinline__ void resample_phase(
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat = nullptr) {
+  constexpr bool INLAUNCH = MODE != 0;
   const int N = fa.N;
   const int blk = blockIdx.x, lane = lane_id(), wv = wave_id();
   const int g = blk / fa.gsz;
@@ -1661,6 +1702,27 @@ __device__ __forceinline__ void resample_phase(
   }
   if (wv != 0) return;
 
+  if (MODE == 2) {  // flat: count partial + one arrival; block 0 waits for every block and finishes
+    if (lane == 0) {
+      int bv = sh.c[0], bi = sh.ci[0];
+      for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
+      st_wt(cpart + blk, pack2(bv, bi));
+      if (stamps) stamp_max(stamps, 5, rt_now());
+      flat_arrive(flat + kFlatCountSet, blk);
+    }
+    if (blk != 0) return;
+    if (!flat_wait(flat + kFlatCountSet, fa.flat_base_c + (uint32_t)fa.nblk)) return;  // abandoned: no record
+    int bv = -1, bi = 0x7fffffff;
+    for (int t = lane; t < fa.nblk; t += 64) {
+      const uint64_t cp = ld_wt(cpart + t);
+      cmb_max(bv, bi, lo32(cp), hi32(cp));
+    }
+    wave_argmax(bv, bi);
+    if (stamps && lane == 0) stamps[6] = rt_now();
+    finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, bi, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+    if (stamps && lane == 0) stamps[7] = rt_now();
+    return;
+  }
   int last = 0;
   if (lane == 0) {
     int bv = sh.c[0], bi = sh.ci[0];
@@ -1735,7 +1797,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
-  resample_phase<T, RNG, MAXM, SP, false>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
+  resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
                                mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
 }
 
@@ -1877,7 +1939,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
     uint32_t* __restrict__ gcount_w, uint32_t* __restrict__ tcount_w, uint32_t* __restrict__ gcount_r,
     uint32_t* __restrict__ tcount_r, uint32_t* __restrict__ gen, uint32_t* __restrict__ counts,
     Cand* __restrict__ cand, double* __restrict__ mlpose,
-    OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+    OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds wsh;
@@ -1976,8 +2038,317 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   }
   const BlockScan bs = fsh.bs[kslot];
   const GroupScan gs = fsh.gs;
-  resample_phase<T, RNG, MAXM, SP, true>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
-                               mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
+  if (flat)  // the count barrier flat (block 0 waits for every arrival), the weighing barrier a tree
+    resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps, flat);
+  else
+    resample_phase<T, RNG, MAXM, SP, 1>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
+}
+
+// ---- the whole frame in ONE launch with FLAT hand-offs (k_frame2; <= 512 co-resident blocks, groups of 64).
+// Weighing barrier: every block stores its partial write-through and makes one arrival on the sharded
+// weighing counters; every block then waits for all arrivals, loads ALL block partials (one round trip)
+// and reduces them itself with exactly the group / top arithmetic of the tree path (propagate_group with
+// one tile, propagate_top's one-tile branch), so no top wave, release word or control-record round trip
+// sits between the weighing pass and the resampling.  Count barrier: one arrival per block; block 0 waits
+// and writes the frame record.  Every wait is bounded (~2 s): an abandoned frame has no record and the
+// host redoes it with two launches.
+struct Frame2Lds {
+  GroupPart gp[2][kFlatMaxGroups];  // group partials per weight slot (the slot's latest iteration)
+  BlockScan bs[2];                  // this block's in-group scan words per slot
+  GroupScan gs;                     // this block's group prefix / running max (kept slot)
+  Ctrl c;
+  int abort;
+};
+
+// propagate_group's arithmetic for a one-tile group (gsz <= 64), from partials in registers; the lane
+// holding block `mine` also returns its scan words
+__device__ __forceinline__ GroupPart group_math_regs(bool vb, double sum, double maxrel, double minrel, double bmaxw,
+                                                     double bminw, int bamax, int bamin, bool mine, BlockScan* own) {
+  double cE = 0.0, cmax = -INFINITY, cmin = INFINITY;
+  double maxw = -INFINITY, minw = INFINITY;
+  int amax = 0x7fffffff, amin = 0x7fffffff;
+  if (vb) {
+    cmb_max(maxw, amax, bmaxw, bamax);
+    cmb_min(minw, amin, bminw, bamin);
+  } else {
+    sum = 0.0;
+    maxrel = -INFINITY;
+    minrel = INFINITY;
+  }
+  const double incl = wave_incl_sum(sum);
+  const double E = cE + wave_shr1(incl, 0.0);
+  const double zmax = vb ? E + maxrel : -INFINITY;
+  const double zmin = vb ? E + minrel : INFINITY;
+  const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
+  double zp_max = wave_shr1(zi_max, -(double)INFINITY), zp_min = wave_shr1(zi_min, (double)INFINITY);
+  zp_max = zp_max > cmax ? zp_max : cmax;
+  zp_min = zp_min < cmin ? zp_min : cmin;
+  if (vb && mine) {
+    own->E = E;
+    own->zin_max = zp_max;
+    own->zin_min = zp_min;
+    own->pad = 0.0;
+  }
+  cE = cE + lane_value(incl, 63);
+  const double tmax = lane_value(zi_max, 63), tmin = lane_value(zi_min, 63);
+  cmax = tmax > cmax ? tmax : cmax;
+  cmin = tmin < cmin ? tmin : cmin;
+  wave_argmax(maxw, amax);
+  wave_argmin(minw, amin);
+  GroupPart r;
+  r.sum = cE;
+  r.zmax = cmax;
+  r.zmin = cmin;
+  r.maxw = maxw;
+  r.minw = minw;
+  r.argmax = amax;
+  r.argmin = amin;
+  return r;
+}
+
+// propagate_top's one-tile arithmetic (<= 64 groups), partials in registers: q0 = this iteration's partial
+// of the lane's group, qk(slot) = the partial of the lane's group in weight slot `slot` (for the kept
+// slot).  Returns the new control record (wave-uniform) and the lane's group G / Gin when done.
+template <typename T, int RNG, typename KeptF>
+__device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, int iter, int slot, const GroupPart& q0,
+                                              KeptF qk, double* G_out, double* Gin_out) {
+  const int lane = lane_id();
+  const int ngrp = fa.ngrp;
+  double mv = q0.maxw;
+  int mi = q0.argmax;
+  wave_argmax(mv, mi);
+  if (mv > c.best_max) {  // strict: PE:608
+    c.best_max = mv;
+    c.best_idx = mi;
+    c.best_iter = iter;
+    c.best_slot = slot;
+    c.has_best = 1;
+  }
+  c.iters = iter + 1;
+  const bool go_on = fa.force_iters > 0 ? (c.iters < fa.force_iters) : (c.iters < fa.max_iter && mv < fa.exit_thr);
+  c.cur_slot = c.has_best ? 1 - c.best_slot : 1 - slot;
+  if (!go_on) {
+    c.done = 1;
+    c.kept_slot = c.has_best ? c.best_slot : slot;
+    c.kept_iter = c.has_best ? c.best_iter : iter;
+    GroupPart kq = q0;
+    if (c.kept_slot != slot) kq = qk(c.kept_slot);
+    double carry = 0.0;
+    {
+      const double sv = lane < ngrp ? kq.sum : 0.0;
+      carry = carry + lane_value(wave_incl_sum(sv), 63);
+    }
+    const double S = carry;
+    double run = -INFINITY;
+    carry = 0.0;
+    {
+      GroupPart q;
+      q.sum = 0.0;
+      q.zmax = -INFINITY;
+      q.zmin = INFINITY;
+      if (lane < ngrp) q = kq;
+      const double incl = wave_incl_sum(q.sum);
+      const double prev = wave_shr1(incl, 0.0);
+      const double G = lane == 0 ? carry : carry + prev;
+      double cm = -INFINITY;
+      if (lane < ngrp && S != 0.0) cm = (G + (S > 0.0 ? q.zmax : q.zmin)) / S;
+      const double im = wave_incl_max(cm);
+      double ex = wave_shr1(im, -(double)INFINITY);
+      ex = ex > run ? ex : run;
+      *G_out = G;
+      *Gin_out = ex;
+      const double tm = lane_value(im, 63);
+      run = tm > run ? tm : run;
+    }
+    if (S == 0.0) run = -INFINITY;
+    double amv = -INFINITY, anv = INFINITY;
+    int ami = 0x7fffffff, ani = 0x7fffffff;
+    if (lane < ngrp) {
+      cmb_max(amv, ami, kq.maxw, kq.argmax);
+      cmb_min(anv, ani, kq.minw, kq.argmin);
+    }
+    wave_argmax(amv, ami);
+    wave_argmin(anv, ani);
+    const double highest = c.has_best ? c.best_max : 0.0;
+    c.S = S;
+    c.Rmax = run;
+    c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
+    if (c.accepted) {
+      c.most_likely_idx = c.best_idx;
+      int64_t kt = lane == 0 ? count_targets<T, RNG>(fa, c.iters, run) : 0;
+      c.K_total = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)kt, 0)) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)kt >> 32), 0) << 32));
+    } else {
+      c.most_likely_idx = (S < 0.0) ? ani : ami;
+      c.K_total = 0;
+    }
+  }
+  return c;
+}
+
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) void k_frame2(
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
+    BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart,
+    uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
+    double* __restrict__ mlpose, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds wsh;
+  __shared__ ResampleLds<T> rsh;
+  __shared__ OutDev rec;
+  __shared__ Frame2Lds fl;
+
+  if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
+  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = n < fa.N;
+  const int lane = lane_id(), wv = wave_id();
+  const int blk = blockIdx.x, g_own = blk / fa.gsz;
+
+  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  T A[12];
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  stage_consts(fa, sc);
+  if (threadIdx.x == 0) {
+    fl.c = zero_ctrl();  // start of frame: every block keeps an identical copy of the control record
+    fl.abort = 0;
+  }
+  __syncthreads();
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  if (stamps && threadIdx.x == 0) {
+    const uint64_t t = rt_now();
+    stamp_max(stamps, 8, t);
+    stamp_min(stamps, 19, t);
+  }
+
+  T P[12], w = (T)0;
+  Ctrl c = fl.c;
+  int iter = 0;
+  for (;; ++iter) {
+    const int slot = c.cur_slot;
+    if (valid) {
+      w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P, nullptr, stamps);
+      (slot ? w1 : w0)[n] = w;
+    }
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
+    // block partial (publish_iteration's block level), one arrival
+    {
+      const double wd = valid ? (double)w : 0.0;
+      const double wi = wave_incl_sum(wd);
+      const double rmx = wave_max(valid ? wi : -INFINITY);
+      const double rmn = wave_min(valid ? wi : INFINITY);
+      T mx = valid ? w : -inf_t<T>(), mn = valid ? w : inf_t<T>();
+      int ix = valid ? n : 0x7fffffff, in_ = ix;
+      wave_argmax(mx, ix);
+      wave_argmin(mn, in_);
+      if (lane == 63) wsh.tot[wv] = wi;
+      if (lane == 0) {
+        wsh.rmax[wv] = rmx;
+        wsh.rmin[wv] = rmn;
+        wsh.mx[wv] = (double)mx;
+        wsh.mn[wv] = (double)mn;
+        wsh.ix[wv] = ix;
+        wsh.in_[wv] = in_;
+      }
+      __syncthreads();
+      if (wv == 0) {
+        if (lane == 0) {
+          double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = wsh.mx[0], bmn = wsh.mn[0];
+          int bix = wsh.ix[0], bin = wsh.in_[0];
+#pragma unroll
+          for (int ww = 0; ww < kWaves; ++ww) {
+            const double a = pre + wsh.rmax[ww], b = pre + wsh.rmin[ww];
+            maxrel = a > maxrel ? a : maxrel;
+            minrel = b < minrel ? b : minrel;
+            if (ww) {
+              cmb_max(bmx, bix, wsh.mx[ww], wsh.ix[ww]);
+              cmb_min(bmn, bin, wsh.mn[ww], wsh.in_[ww]);
+            }
+            pre = pre + wsh.tot[ww];
+          }
+          BlockPart* bp = (slot ? part1 : part0) + blk;
+          st_wt_d(&bp->sum, pre);
+          st_wt_d(&bp->maxrel, maxrel);
+          st_wt_d(&bp->minrel, minrel);
+          st_wt_d(&bp->maxw, bmx);
+          st_wt_d(&bp->minw, bmn);
+          st_wt(&bp->argmax, pack2(bix, bin));
+          if (stamps) stamp_max(stamps, 1, rt_now());
+          flat_arrive(flat, blk);
+        }
+        const uint32_t target = fa.flat_base_w + (uint32_t)(iter + 1) * (uint32_t)fa.nblk;
+        const bool ok = flat_wait(flat, target);
+        if (lane == 0 && !ok) fl.abort = 1;
+      }
+      __syncthreads();
+      if (fl.abort) return;
+    }
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 2, rt_now());
+    // every block: the group partials (wave w: groups w, w + 4) from all block partials, then the top
+    for (int g = wv; g < fa.ngrp; g += kWaves) {
+      const int b = g * fa.gsz + lane;
+      const bool vb = lane < fa.gsz && b < fa.nblk;
+      double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY, maxw = -INFINITY, minw = INFINITY;
+      int amax = 0x7fffffff, amin = 0x7fffffff;
+      if (vb) {
+        const BlockPart* p = (slot ? part1 : part0) + b;
+        sum = ld_wt_d(&p->sum);
+        maxrel = ld_wt_d(&p->maxrel);
+        minrel = ld_wt_d(&p->minrel);
+        maxw = ld_wt_d(&p->maxw);
+        minw = ld_wt_d(&p->minw);
+        const uint64_t ai = ld_wt(&p->argmax);
+        amax = lo32(ai);
+        amin = hi32(ai);
+      }
+      const GroupPart r = group_math_regs(vb, sum, maxrel, minrel, maxw, minw, amax, amin, b == blk, &fl.bs[slot]);
+      if (lane == 0) fl.gp[slot][g] = r;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      GroupPart q0;
+      q0.sum = 0.0;
+      q0.zmax = -INFINITY;
+      q0.zmin = INFINITY;
+      q0.maxw = -INFINITY;
+      q0.minw = INFINITY;
+      q0.argmax = q0.argmin = 0x7fffffff;
+      if (lane < fa.ngrp) q0 = fl.gp[slot][lane];
+      auto qk = [&](int ks) {
+        GroupPart q = q0;
+        if (lane < fa.ngrp) q = fl.gp[ks][lane];
+        return q;
+      };
+      double G = 0.0, Gin = -INFINITY;
+      const Ctrl cn = top_math_regs<T, RNG>(fa, c, iter, slot, q0, qk, &G, &Gin);
+      if (lane == g_own) {
+        fl.gs.G = G;
+        fl.gs.Gin = Gin;
+      }
+      if (lane == 0) fl.c = cn;
+    }
+    __syncthreads();
+    c = fl.c;
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 3, rt_now());
+    if (c.done) break;
+  }
+
+  if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
+    if (blk == 0 && wv == 0)
+      finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
+    return;
+  }
+  const int kslot = c.kept_slot;
+  const bool have_P = c.kept_iter == iter;
+  double wd = 0.0;
+  if (valid) wd = have_P ? (double)w : (double)(kslot ? w1 : w0)[n];
+  const BlockScan bs = fl.bs[kslot];
+  const GroupScan gs = fl.gs;
+  resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
+                                      mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq, stamps, flat);
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path).  anchor: the set's

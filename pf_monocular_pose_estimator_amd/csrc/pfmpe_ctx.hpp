@@ -69,7 +69,9 @@ struct pfmpe_ctx {
   void* h_det = nullptr;           // detector output record (pinned, host-mapped)
   int num_cu = 0;
   bool coop = false;               // device supports cooperative launches
-  bool fused = true;               // PFMPE_OPT_FUSED
+  int fused = 2;                   // PFMPE_OPT_FUSED: 2 flat one-launch (k_frame2), 1 tree (k_frame), 0 two launches
+  uint32_t* d_flat = nullptr;      // k_frame2 sharded arrival counters (kFlatWords)
+  uint32_t flat_base_w = 0, flat_base_c = 0;  // their running totals (host mirror)
   int64_t fused_fallbacks = 0;     // fused frames redone with two launches
   std::map<std::pair<const void*, size_t>, int> occ;  // (kernel, LDS bytes) -> blocks per CU
   Ctrl* d_ctrl = nullptr;
@@ -257,12 +259,14 @@ struct Seq {
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;
   }
-  // the whole frame as one cooperative launch, if every block can be resident at once
+  // the whole frame as one launch, if every block can be resident at once: k_frame2 (flat hand-offs,
+  // c->fused == 2, <= 512 blocks) or k_frame (tree hand-offs)
   template <bool PRUNE>
-  static int frame_fused(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, bool* launched) {
+  static int frame_fused(pfmpe_ctx* c, const FrameArgsT<T>& fa_in, const unsigned char* table, bool* launched) {
     *launched = false;
-    const void* fn = (const void*)k_frame<T, RNG, MAXM, PRUNE, SP>;
-    const size_t lds = BlobTable<T>::bytes(fa.B);
+    const bool flat = c->fused == 2 && fa_in.nblk <= kFlatMaxGroups * kGroup && fa_in.gsz == kGroup && c->d_flat;
+    const void* fn = flat ? (const void*)k_frame2<T, RNG, MAXM, PRUNE, SP> : (const void*)k_frame<T, RNG, MAXM, PRUNE, SP>;
+    const size_t lds = BlobTable<T>::bytes(fa_in.B);
     auto key = std::make_pair(fn, lds);
     auto it = c->occ.find(key);
     if (it == c->occ.end()) {
@@ -275,7 +279,10 @@ struct Seq {
     // cooperative launch would only add this check at +15-19 us per frame (MI355X_MICROARCH.md
     // "coop-launch"); every in-kernel wait is bounded anyway.
     const int per_cu = std::min(2, it->second - 1);
-    if (per_cu < 1 || (int64_t)per_cu * c->num_cu < fa.nblk) return PFMPE_OK;  // two-launch path
+    if (per_cu < 1 || (int64_t)per_cu * c->num_cu < fa_in.nblk) return PFMPE_OK;  // two-launch path
+    FrameArgsT<T> a = fa_in;
+    a.flat_base_w = c->flat_base_w;
+    a.flat_base_c = c->flat_base_c;
     const SP* prior = (const SP*)c->d_state[c->prior_idx];
     SP* post = (SP*)c->d_state[1 - c->prior_idx];
     T* w0 = (T*)c->d_w[0];
@@ -287,13 +294,17 @@ struct Seq {
     uint32_t* counts = c->record_counts ? c->d_counts : nullptr;
     c->seq = (c->seq + 1) & 0x3fffffff;
     int32_t seq = c->seq;
-    const FrameArgsT<T> a = fa;
     RET(launch(c, PFMPE_K_FRAME, [&] {
-      hipLaunchKernelGGL((k_frame<T, RNG, MAXM, PRUNE, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, a, table,
-                         prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
-                         c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
-                         tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
-                         c->d_stamps);
+      if (flat)
+        hipLaunchKernelGGL((k_frame2<T, RNG, MAXM, PRUNE, SP>), dim3(a.nblk), dim3(kBlock), lds, c->stream, a, table,
+                           prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_ctrl, c->d_cpart, c->d_flat, counts,
+                           c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps);
+      else
+        hipLaunchKernelGGL((k_frame<T, RNG, MAXM, PRUNE, SP>), dim3(a.nblk), dim3(kBlock), lds, c->stream, a, table,
+                           prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
+                           c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
+                           tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
+                           c->d_stamps, (c->diag & 16) ? nullptr : c->d_flat);
     }));
     *launched = true;
     if (wait_frame(c) != PFMPE_OK) {
@@ -302,10 +313,18 @@ struct Seq {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
+      if (c->d_flat) HIPCHK(c, hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      c->flat_base_w = c->flat_base_c = 0;
       c->fused_fallbacks += 1;
-      c->fused = false;
+      c->fused = 0;
       *launched = false;
       return PFMPE_OK;
+    }
+    if (flat || !(c->diag & 16)) {  // the flat counters' new running totals (k_frame: the count set only)
+      const OutDev& o = *(const OutDev*)c->h_out;
+      if (flat) c->flat_base_w += (uint32_t)o.iters * (uint32_t)a.nblk;
+      if (o.resampled) c->flat_base_c += (uint32_t)a.nblk;
     }
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));
     return PFMPE_OK;
@@ -429,7 +448,11 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   fa.max_iter = p.max_iter;
   fa.force_iters = in->force_iters;
   fa.nblk = (c->N + kBlock - 1) / kBlock;
-  fa.gsz = std::min(kGroup, std::max(1, (int)std::ceil(std::sqrt((double)std::max(1, fa.nblk)))));
+  // groups of 64 whenever the frame can run as one flat launch (k_frame2 reduces one group per wave), so
+  // the one-launch and two-launch shapes keep the same summation association; ~sqrt(nblk) beyond
+  fa.gsz = (fa.nblk <= kFlatMaxGroups * kGroup && !(c->diag & 32))
+               ? kGroup
+               : std::min(kGroup, std::max(1, (int)std::ceil(std::sqrt((double)std::max(1, fa.nblk)))));
   fa.ngrp = (fa.nblk + fa.gsz - 1) / fa.gsz;
   // (c->max_grp = max_blk >= ngrp for every N <= max_particles)
   fa.diag = c->diag;

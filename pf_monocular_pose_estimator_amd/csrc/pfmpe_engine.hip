@@ -81,7 +81,7 @@ void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* 
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
-                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -162,6 +162,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_gen, sizeof(uint32_t)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_cand, (size_t)c->max_blk * sizeof(Cand)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_mlpose, 12 * sizeof(double)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_flat, kFlatWords * sizeof(uint32_t)) == hipSuccess;
   ok = ok && hipMemset(c->d_gen, 0, sizeof(uint32_t)) == hipSuccess;
   {
     int coop = 0;
@@ -177,6 +178,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   if (hipMemset(c->d_ctrl, 0, sizeof(Ctrl)) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand)) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_counters, 0, counters_bytes(c)) != hipSuccess) return bad(PFMPE_E_HIP);
+  if (hipMemset(c->d_flat, 0, kFlatWords * sizeof(uint32_t)) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_state[0], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
   if (hipMemset(c->d_state[1], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
   *out = c;
@@ -230,7 +232,8 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       }
       return PFMPE_OK;
     case PFMPE_OPT_FUSED:
-      c->fused = value != 0;
+      if (value < 0 || value > 2) return fail(c, PFMPE_E_ARG, "set_option: FUSED is 0, 1 or 2");
+      c->fused = (int)value;
       return PFMPE_OK;
     case PFMPE_OPT_PRUNE:
       c->prune = value != 0;

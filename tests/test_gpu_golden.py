@@ -19,7 +19,7 @@ INT_KEYS = ("iters", "kept_iter", "accepted", "resampled", "most_likely_idx", "w
 
 @pytest.mark.parametrize("name", STREAMS)
 @pytest.mark.parametrize("bank", [False, True])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_engine_reproduces_fixture(name, bank, fused):
     g = dict(np.load(os.path.join(GOLDEN, name + ".npz")))
     N = g["prior0"].shape[0]
@@ -29,7 +29,7 @@ def test_engine_reproduces_fixture(name, bank, fused):
     prm.rng_mode = int(g["rng_mode"])
     eng.set_params(prm)
     eng.set_option(pf.OPT_RECORD_COUNTS, 1)
-    eng.set_option(pf.OPT_FUSED, 1 if fused else 0)
+    eng.set_option(pf.OPT_FUSED, int(fused))
     eng.set_prior(g["prior0"])
     nf = len(g["seed"])
     if bank:

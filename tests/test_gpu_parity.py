@@ -21,9 +21,9 @@ RNG = {"ref": pf.RNG_REFERENCE, "philox": pf.RNG_PHILOX}
 STATE = {"f64": pf.STATE_F64, "f32": pf.STATE_F32, "f16": pf.STATE_F16}
 
 
-def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None, fused=True):
+def make_engine(N, markers, K, state, rng, prune=True, downgrade=None, params=None, fused=2):
     eng = pf.Engine(device=0, max_particles=max(N, 1), state_dtype=state)
-    eng.set_option(pf.OPT_FUSED, 1 if fused else 0)  # one cooperative launch per frame / two launches
+    eng.set_option(pf.OPT_FUSED, int(fused))  # 2 flat / 1 tree one-launch frame, 0 two launches
     eng.set_model(markers, K, downgrade)
     prm = params or pf.default_params()
     prm.rng_mode = rng
@@ -79,7 +79,7 @@ CASES = [  # (N, M, B, heavy)
 @pytest.mark.parametrize("rng", ["ref", "philox"])
 @pytest.mark.parametrize("N,M,B,heavy", CASES)
 @pytest.mark.parametrize("prune", [True, False])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune, fused):
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 3)
@@ -98,7 +98,7 @@ def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune, fused):
 
 
 @pytest.mark.parametrize("rng", ["ref", "philox"])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_fp64_exit_rule_runs_all_iterations(rng, fused):
     """One LED occluded -> max weight < M*min(5,B): the loop runs all 80 iterations with noise growth
     and keeps the earliest strictly-best iteration (PE:606-624)."""
@@ -123,7 +123,7 @@ def test_fp64_exit_rule_runs_all_iterations(rng, fused):
 
 @pytest.mark.parametrize("state", ["f64", "f32"])
 @pytest.mark.parametrize("N", [1, 2, 3, 257])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_small_particle_counts(state, N, fused):
     cfg = syn.StreamConfig("t", M=5, B=20, N=N)
     st = syn.make_stream(cfg, 2)
@@ -145,7 +145,7 @@ def test_small_particle_counts(state, N, fused):
 
 
 @pytest.mark.parametrize("state", ["f64", "f32"])
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_no_blobs_reinitialises(state, fused):
     N = 300
     cfg = syn.StreamConfig("t", M=5, B=20, N=N)
@@ -409,7 +409,7 @@ def test_fp64_exact_multi_group(rng):
     eng.close()
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_fp16_state(fused):
     """fp16-delta state (BASELINE.json configs[3]): per frame the oracle starts from the engine's own
     dequantised prior, so propagation/weights match as in fp32; the resampled set equals the selected
