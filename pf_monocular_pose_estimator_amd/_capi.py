@@ -142,7 +142,7 @@ def load() -> C.CDLL:
         raise RuntimeError(
             f"{LIB_PATH} is missing: build the HIP engine first (python -c 'import __graft_entry__ as g; g.build()')"
         )
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(os.environ.get("PFMPE_LIB_OVERRIDE") or LIB_PATH)  # override: A/B builds of the same ABI
     P, I, D, U64, I64 = C.c_void_p, C.c_int, C.c_double, C.c_uint64, C.c_int64
     dp = C.POINTER(C.c_double)
     sig = {

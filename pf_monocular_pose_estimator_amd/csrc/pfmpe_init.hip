@@ -26,6 +26,9 @@ using namespace pfmpe_impl;
 namespace pfmpe {
 
 constexpr int kInitBlock = 256;
+#ifndef PFMPE_P3P_MINB
+#define PFMPE_P3P_MINB 2  // 2 waves per SIMD: 353 us vs 519 us at 1 (scratch 160 B vs 80 B), 476 us at 3 (spills)
+#endif
 constexpr double kThreshDist = 10000 * 100;  // threshDist / threshDist2 (PE:1557-1558), px^2
 
 struct InitArgs {
@@ -128,7 +131,7 @@ __global__ void k_p3p_filter(const InitArgs ia, const double* __restrict__ blobs
 // LDS (flushed once per block with integer atomics) or straight to global atomics for large B x M.
 // Dynamic LDS: sorted blob x, y (doubles), original index (int), then the LDS histogram.
 template <int MAXU, bool HLDS>
-__global__ __launch_bounds__(kInitBlock) void k_p3p_hist(const InitArgs ia, const double* __restrict__ blobs,
+__global__ __launch_bounds__(kInitBlock, PFMPE_P3P_MINB) void k_p3p_hist(const InitArgs ia, const double* __restrict__ blobs,
                                                           const double* __restrict__ iv,
                                                           const double* __restrict__ sorted_xy,
                                                           const int* __restrict__ sorted_idx,
