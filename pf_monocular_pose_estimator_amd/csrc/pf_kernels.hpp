@@ -135,6 +135,17 @@ struct OutDev {
   int32_t kept_slot;
   int32_t tag;
 };
+// The record as the kernel publishes it: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1"), 8-byte
+// words {OutDev word k (low 32 bits), tag (high 32)}, each ONE relaxed system-scope store, so the host has
+// the whole record once every granule carries the current tag, and the final wave needs no release (no
+// wait for the PCIe write acknowledgements).  An unfinished iteration batch (two-launch path) writes
+// granule 0 alone, with tag 2 * seq.
+constexpr int kRecWords = (int)(offsetof(OutDev, tag) / 4);
+constexpr int kRecGran = 128;
+static_assert(offsetof(OutDev, tag) % 4 == 0 && kRecWords <= kRecGran && kRecWords > 64, "record granules");
+struct RecOut {
+  uint64_t g[kRecGran];
+};
 
 // ----------------------------------------------------------------------------- scalar helpers
 __device__ __forceinline__ float fmadd(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -571,6 +582,14 @@ __device__ __forceinline__ double dpp(double src, double old) {
   return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 // value of lane L in every lane (scalar result)
+// A value the optimiser may not look through.  In a select chain over a register array (lane q picks word
+// q) the loads would otherwise be folded into ONE load of a selected address, which pins the array in
+// scratch memory (a VMEM round trip per use); with the values opaque the chain stays v_cndmask.
+template <typename V>
+__device__ __forceinline__ V opaque(V x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 __device__ __forceinline__ int lane_value(int x, int L) { return __builtin_amdgcn_readlane(x, L); }
 __device__ __forceinline__ float lane_value(float x, int L) {
   return __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(x), L));
@@ -617,19 +636,18 @@ __device__ __forceinline__ double wave_max(double v) { return lane_value(wave_in
 __device__ __forceinline__ double wave_min(double v) { return lane_value(wave_incl_min(v), 63); }
 
 // (value, index): larger value wins, lower index on ties
+// (selects, not branches: the wave reductions stay one basic block)
 template <typename V>
 __device__ __forceinline__ void cmb_max(V& v, int& i, V v2, int i2) {
-  if (v2 > v || (v2 == v && i2 < i)) {
-    v = v2;
-    i = i2;
-  }
+  const bool t = (v2 > v) | ((v2 == v) & (i2 < i));  // non-short-circuit: no exec-mask branches
+  v = t ? v2 : v;
+  i = t ? i2 : i;
 }
 template <typename V>
 __device__ __forceinline__ void cmb_min(V& v, int& i, V v2, int i2) {
-  if (v2 < v || (v2 == v && i2 < i)) {
-    v = v2;
-    i = i2;
-  }
+  const bool t = (v2 < v) | ((v2 == v) & (i2 < i));
+  v = t ? v2 : v;
+  i = t ? i2 : i;
 }
 // wave arg-reductions: the lexicographic (value, index) order is associative and commutative, so the
 // scan pattern reduces it exactly; the result is broadcast to every lane
@@ -697,6 +715,54 @@ __device__ __forceinline__ void block_incl_sum(double v, double& incl, double* s
   incl = pre + wi;
 }
 
+// ---- interleaved wave scans: several independent chains advanced step by step in ONE basic block, so
+// the DPP / f64 latencies of one chain hide behind the others.  Each chain's arithmetic is exactly that
+// of wave_scan / wave_argmax / wave_argmin (same steps, same identities, same operand order).
+template <int C, int R>
+struct DppStep {
+  static constexpr int ctrl = C, rm = R;
+};
+template <typename F>
+__device__ __forceinline__ void scan_steps(F&& f) {
+  f(DppStep<kDppRowShr1, 0xf>{});
+  f(DppStep<kDppRowShr2, 0xf>{});
+  f(DppStep<kDppRowShr4, 0xf>{});
+  f(DppStep<kDppRowShr8, 0xf>{});
+  f(DppStep<kDppBcast15, 0xa>{});
+  f(DppStep<kDppBcast31, 0xc>{});
+}
+template <typename S>
+__device__ __forceinline__ void st_sum(double& x) {
+  x = x + dpp<S::ctrl, S::rm>(x, 0.0);
+}
+template <typename S>
+__device__ __forceinline__ void st_max(double& x) {
+  const double y = dpp<S::ctrl, S::rm>(x, -(double)INFINITY);
+  x = y > x ? y : x;
+}
+template <typename S>
+__device__ __forceinline__ void st_min(double& x) {
+  const double y = dpp<S::ctrl, S::rm>(x, (double)INFINITY);
+  x = y < x ? y : x;
+}
+template <typename S, typename V>
+__device__ __forceinline__ void st_argmax(V& v, int& i) {
+  const V v2 = dpp<S::ctrl, S::rm>(v, -(V)INFINITY);
+  const int i2 = dpp<S::ctrl, S::rm>(i, 0x7fffffff);
+  cmb_max(v, i, v2, i2);
+}
+template <typename S, typename V>
+__device__ __forceinline__ void st_argmin(V& v, int& i) {
+  const V v2 = dpp<S::ctrl, S::rm>(v, (V)INFINITY);
+  const int i2 = dpp<S::ctrl, S::rm>(i, 0x7fffffff);
+  cmb_min(v, i, v2, i2);
+}
+template <typename V>
+__device__ __forceinline__ void bcast63(V& v, int& i) {
+  v = lane_value(v, 63);
+  i = lane_value(i, 63);
+}
+
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
 template <typename T, int RNG>
@@ -758,16 +824,9 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
 typedef __attribute__((address_space(1))) uint64_t gu64_t;
 typedef __attribute__((address_space(1))) uint32_t gu32_t;
 
-// publication to the host (HIP memory model, system scope): relaxed write-through stores of the record,
-// then ONE release store of the tag
+// publication to the host: relaxed system-scope stores of tagged 8-byte granules (RecOut)
 __device__ __forceinline__ void st_sys64(void* p, uint64_t v) {
   __hip_atomic_store((gu64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys32(void* p, uint32_t v) {
-  __hip_atomic_store((gu32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void publish_tag(int32_t* p, int32_t tag) {
-  __hip_atomic_store((gu32_t*)p, (uint32_t)tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void st_wt(void* p, uint64_t v) {
@@ -778,6 +837,30 @@ __device__ __forceinline__ uint64_t ld_wt(const void* p) {
   return __hip_atomic_load((gu64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ double ld_wt_d(const double* p) { return __longlong_as_double((long long)ld_wt(p)); }
+// a whole BlockPart as three 16-B write-through-coherent (sc1) loads, issued without waiting.  The raw
+// registers are asm outputs; wait_parts drains vmcnt with them as in/out operands, so no use of them can
+// be scheduled before the wait.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+struct PartRaw {
+  u32x4_t a, b, c;
+};
+__device__ __forceinline__ void ld_part_issue(const BlockPart* p, PartRaw& r) {
+  static_assert(sizeof(BlockPart) == 48, "BlockPart is three 16-B granules");
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r.a) : "v"((const char*)p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:16 sc1" : "=v"(r.b) : "v"((const char*)p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off offset:32 sc1" : "=v"(r.c) : "v"((const char*)p) : "memory");
+}
+__device__ __forceinline__ void wait_parts(PartRaw& r0, PartRaw& r1) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(r0.a), "+v"(r0.b), "+v"(r0.c), "+v"(r1.a), "+v"(r1.b), "+v"(r1.c)::"memory");
+}
+__device__ __forceinline__ BlockPart unpack_part(const PartRaw& r) {
+  BlockPart q;
+  u32x4_t* d = (u32x4_t*)&q;
+  d[0] = r.a;
+  d[1] = r.b;
+  d[2] = r.c;
+  return q;
+}
 __device__ __forceinline__ uint64_t pack2(int a, int b) { return (uint64_t)(uint32_t)a | ((uint64_t)(uint32_t)b << 32); }
 __device__ __forceinline__ int lo32(uint64_t v) { return (int)(uint32_t)v; }
 __device__ __forceinline__ int hi32(uint64_t v) { return (int)(uint32_t)(v >> 32); }
@@ -1204,6 +1287,36 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
   return w;
 }
 
+// A wave's weight partials (the wave-inclusive scan wi of the weights, the extrema of wi over valid lanes,
+// max / argmax and min / argmin of the weights), the independent chains interleaved; the extrema and
+// arg results are wave-uniform
+template <typename T>
+__device__ __forceinline__ void wave_weight_partials(T w, bool valid, int n, double& wi, double& rmx, double& rmn,
+                                                     T& mx, int& ix, T& mn, int& in_) {
+  wi = valid ? (double)w : 0.0;
+  mx = valid ? w : -inf_t<T>();
+  mn = valid ? w : inf_t<T>();
+  ix = valid ? n : 0x7fffffff;
+  in_ = ix;
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_sum<S>(wi);
+    st_argmax<S>(mx, ix);
+    st_argmin<S>(mn, in_);
+  });
+  bcast63(mx, ix);
+  bcast63(mn, in_);
+  rmx = valid ? wi : -INFINITY;
+  rmn = valid ? wi : INFINITY;
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_max<S>(rmx);
+    st_min<S>(rmn);
+  });
+  rmx = lane_value(rmx, 63);
+  rmn = lane_value(rmn, 63);
+}
+
 // LDS scratch of the per-iteration partials
 struct WeighLds {
   double tot[kWaves], rmax[kWaves], rmin[kWaves], mx[kWaves], mn[kWaves];
@@ -1222,14 +1335,10 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
                                                   uint32_t* __restrict__ tcount, uint32_t* __restrict__ gen,
                                                   uint32_t gen_base, uint64_t* __restrict__ stamps) {
   // wave partials: scan total, extrema of the wave-inclusive prefix, max/argmax, min/argmin
-  const double wd = valid ? (double)w : 0.0;
-  const double wi = wave_incl_sum(wd);
-  const double rmx = wave_max(valid ? wi : -INFINITY);
-  const double rmn = wave_min(valid ? wi : INFINITY);
-  T mx = valid ? w : -inf_t<T>(), mn = valid ? w : inf_t<T>();
-  int ix = valid ? n : 0x7fffffff, in_ = ix;
-  wave_argmax(mx, ix);
-  wave_argmin(mn, in_);
+  double wi, rmx, rmn;
+  T mx, mn;
+  int ix, in_;
+  wave_weight_partials(w, valid, n, wi, rmx, rmn, mx, ix, mn, in_);
   const int lane = lane_id(), wv = wave_id();
   if (lane == 63) sh.tot[wv] = wi;
   if (lane == 0) {
@@ -1362,8 +1471,8 @@ __device__ __forceinline__ int pairs_from_minima(const FrameArgsT<T>& fa, const 
     int rj = 0;
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
-      mj = (lane == j && j < M) ? m[j] : mj;
-      rj = lane == j ? r[j] : rj;
+      mj = (lane == j && j < M) ? opaque(m[j]) : mj;
+      rj = lane == j ? opaque(r[j]) : rj;
     }
     int rank = 0;
 #pragma unroll
@@ -1432,7 +1541,7 @@ template <typename T, int RNG, int MAXM, typename SP>
 __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c,
                                                Ctrl* __restrict__ ctrl, const SP* __restrict__ prior, int winner,
                                                const Cand* __restrict__ cand, const double* __restrict__ mlpose,
-                                               OutDev& rec, OutDev* __restrict__ out, int32_t tag,
+                                               OutDev& rec, RecOut* __restrict__ out, int32_t tag,
                                                uint64_t* __restrict__ stamps, bool have_pl = false,
                                                uint32_t pl_reg = 0u, double ml_reg = 0.0) {
   const int lane = lane_id();
@@ -1463,7 +1572,7 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
     if (lane < 12) {  // lane q writes pose word q (selects, no dynamic register indexing)
       T pm = Q[0];
 #pragma unroll
-      for (int q = 1; q < 12; ++q) pm = lane == q ? Q[q] : pm;
+      for (int q = 1; q < 12; ++q) pm = lane == q ? opaque(Q[q]) : pm;
       rec.most_likely_pose[lane] = (double)pm;
       rec.winner_pose[lane] = (double)pm;
     }
@@ -1485,12 +1594,11 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
     if (stamps) stamps[17] = rt_now();
   }
   wave_lds_sync();
-  constexpr int kWords = (int)(offsetof(OutDev, kept_slot) / 8);
-  static_assert(offsetof(OutDev, kept_slot) % 8 == 0 && kWords <= 64, "record layout");
-  if (lane < kWords) st_sys64((uint64_t*)out + lane, ((const uint64_t*)&rec)[lane]);
-  if (lane == kWords) st_sys32(&out->kept_slot, (uint32_t)rec.kept_slot);
+  const uint32_t* rw = (const uint32_t*)&rec;
+  const uint64_t th = (uint64_t)(uint32_t)tag << 32;
+  st_sys64(&out->g[lane], th | rw[lane]);
+  if (lane + 64 < kRecWords) st_sys64(&out->g[lane + 64], th | rw[lane + 64]);
   if (lane != 0) return;
-  publish_tag(&out->tag, tag);
   if (stamps) stamps[18] = rt_now();
   // the next frame starts from the all-zero control record
   store_ctrl_wt(ctrl, zero_ctrl());
@@ -1505,7 +1613,7 @@ __device__ __forceinline__ uint32_t payload_word(const T* Pc, const uint32_t* cc
   if (lane < 24) {
     T pv = Pc[0];
 #pragma unroll
-    for (int q = 1; q < 12; ++q) pv = (lane >> 1) == q ? Pc[q] : pv;
+    for (int q = 1; q < 12; ++q) pv = (lane >> 1) == q ? opaque(Pc[q]) : pv;
     const uint64_t bits = (uint64_t)__double_as_longlong((double)pv);
     pl = (lane & 1) ? (uint32_t)(bits >> 32) : (uint32_t)bits;
   } else if (lane < 24 + 2 * kMaxMarkers) {
@@ -1550,7 +1658,7 @@ __device__ __forceinline__ void resample_phase(
     const T* P_in, bool have_P, const BlockScan& bs, const GroupScan& gs, ResampleLds<T>& sh, OutDev& rec,
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
-    uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, OutDev* __restrict__ out, int32_t seq,
+    uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, RecOut* __restrict__ out, int32_t seq,
     uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat = nullptr) {
   constexpr bool INLAUNCH = MODE != 0;
   const int N = fa.N;
@@ -1766,7 +1874,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
-    uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, OutDev* __restrict__ out,
+    uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
     int32_t seq, uint64_t* __restrict__ stamps) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
@@ -1809,7 +1917,7 @@ template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
     const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
-    const double* __restrict__ mlpose, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+    const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the blob table
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
@@ -1852,7 +1960,7 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
     }
   }
   if (!c.done) {
-    if (threadIdx.x == 0) publish_tag(&out->tag, 2 * seq);
+    if (threadIdx.x == 0) st_sys64(&out->g[0], (uint64_t)(uint32_t)(2 * seq) << 32);
     return;
   }
   __syncthreads();  // partials, table and constants
@@ -1939,7 +2047,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
     uint32_t* __restrict__ gcount_w, uint32_t* __restrict__ tcount_w, uint32_t* __restrict__ gcount_r,
     uint32_t* __restrict__ tcount_r, uint32_t* __restrict__ gen, uint32_t* __restrict__ counts,
     Cand* __restrict__ cand, double* __restrict__ mlpose,
-    OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat) {
+    RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds wsh;
@@ -2062,50 +2170,76 @@ struct Frame2Lds {
   int abort;
 };
 
-// propagate_group's arithmetic for a one-tile group (gsz <= 64), from partials in registers; the lane
-// holding block `mine` also returns its scan words
-__device__ __forceinline__ GroupPart group_math_regs(bool vb, double sum, double maxrel, double minrel, double bmaxw,
-                                                     double bminw, int bamax, int bamin, bool mine, BlockScan* own) {
-  double cE = 0.0, cmax = -INFINITY, cmin = INFINITY;
-  double maxw = -INFINITY, minw = INFINITY;
-  int amax = 0x7fffffff, amin = 0x7fffffff;
-  if (vb) {
-    cmb_max(maxw, amax, bmaxw, bamax);
-    cmb_min(minw, amin, bminw, bamin);
-  } else {
-    sum = 0.0;
-    maxrel = -INFINITY;
-    minrel = INFINITY;
+// propagate_group's arithmetic for one-tile groups (gsz = 64), TWO groups per wave (the thread's blocks
+// t and t + 256), their chains interleaved; the lane holding block `mine` also returns its scan words
+struct BlockIn {
+  bool vb, mine;
+  BlockPart p;
+};
+__device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&out)[2], BlockScan* own) {
+  double sum[2], maxrel[2], minrel[2], maxw[2], minw[2];
+  int amax[2], amin[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const bool vb = in[k].vb;
+    maxw[k] = -INFINITY;
+    minw[k] = INFINITY;
+    amax[k] = amin[k] = 0x7fffffff;
+    if (vb) {
+      cmb_max(maxw[k], amax[k], in[k].p.maxw, in[k].p.argmax);
+      cmb_min(minw[k], amin[k], in[k].p.minw, in[k].p.argmin);
+    }
+    sum[k] = vb ? in[k].p.sum : 0.0;
+    maxrel[k] = vb ? in[k].p.maxrel : -INFINITY;
+    minrel[k] = vb ? in[k].p.minrel : INFINITY;
   }
-  const double incl = wave_incl_sum(sum);
-  const double E = cE + wave_shr1(incl, 0.0);
-  const double zmax = vb ? E + maxrel : -INFINITY;
-  const double zmin = vb ? E + minrel : INFINITY;
-  const double zi_max = wave_incl_max(zmax), zi_min = wave_incl_min(zmin);
-  double zp_max = wave_shr1(zi_max, -(double)INFINITY), zp_min = wave_shr1(zi_min, (double)INFINITY);
-  zp_max = zp_max > cmax ? zp_max : cmax;
-  zp_min = zp_min < cmin ? zp_min : cmin;
-  if (vb && mine) {
-    own->E = E;
-    own->zin_max = zp_max;
-    own->zin_min = zp_min;
-    own->pad = 0.0;
+  double incl[2] = {sum[0], sum[1]};
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_sum<S>(incl[0]);
+    st_sum<S>(incl[1]);
+    st_argmax<S>(maxw[0], amax[0]);
+    st_argmax<S>(maxw[1], amax[1]);
+    st_argmin<S>(minw[0], amin[0]);
+    st_argmin<S>(minw[1], amin[1]);
+  });
+  double E[2], zi_max[2], zi_min[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    E[k] = 0.0 + wave_shr1(incl[k], 0.0);
+    zi_max[k] = in[k].vb ? E[k] + maxrel[k] : -INFINITY;
+    zi_min[k] = in[k].vb ? E[k] + minrel[k] : INFINITY;
   }
-  cE = cE + lane_value(incl, 63);
-  const double tmax = lane_value(zi_max, 63), tmin = lane_value(zi_min, 63);
-  cmax = tmax > cmax ? tmax : cmax;
-  cmin = tmin < cmin ? tmin : cmin;
-  wave_argmax(maxw, amax);
-  wave_argmin(minw, amin);
-  GroupPart r;
-  r.sum = cE;
-  r.zmax = cmax;
-  r.zmin = cmin;
-  r.maxw = maxw;
-  r.minw = minw;
-  r.argmax = amax;
-  r.argmin = amin;
-  return r;
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_max<S>(zi_max[0]);
+    st_max<S>(zi_max[1]);
+    st_min<S>(zi_min[0]);
+    st_min<S>(zi_min[1]);
+  });
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    double zp_max = wave_shr1(zi_max[k], -(double)INFINITY), zp_min = wave_shr1(zi_min[k], (double)INFINITY);
+    zp_max = zp_max > -INFINITY ? zp_max : -INFINITY;
+    zp_min = zp_min < INFINITY ? zp_min : INFINITY;
+    if (in[k].vb && in[k].mine) {
+      own->E = E[k];
+      own->zin_max = zp_max;
+      own->zin_min = zp_min;
+      own->pad = 0.0;
+    }
+    const double tmax = lane_value(zi_max[k], 63), tmin = lane_value(zi_min[k], 63);
+    bcast63(maxw[k], amax[k]);
+    bcast63(minw[k], amin[k]);
+    GroupPart& r = out[k];
+    r.sum = 0.0 + lane_value(incl[k], 63);
+    r.zmax = tmax > -INFINITY ? tmax : -INFINITY;
+    r.zmin = tmin < INFINITY ? tmin : INFINITY;
+    r.maxw = maxw[k];
+    r.minw = minw[k];
+    r.argmax = amax[k];
+    r.argmin = amin[k];
+  }
 }
 
 // propagate_top's one-tile arithmetic (<= 64 groups), partials in registers: q0 = this iteration's partial
@@ -2116,9 +2250,27 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
                                               KeptF qk, double* G_out, double* Gin_out) {
   const int lane = lane_id();
   const int ngrp = fa.ngrp;
+  // the exit test's argmax, and speculatively the kept-slot chains for kept slot == this slot (the kept
+  // iteration is an earlier one only when that one holds the best weight): all four interleaved
   double mv = q0.maxw;
   int mi = q0.argmax;
-  wave_argmax(mv, mi);
+  double incl = lane < ngrp ? q0.sum : 0.0;
+  double amv = -INFINITY, anv = INFINITY;
+  int ami = 0x7fffffff, ani = 0x7fffffff;
+  if (lane < ngrp) {
+    cmb_max(amv, ami, q0.maxw, q0.argmax);
+    cmb_min(anv, ani, q0.minw, q0.argmin);
+  }
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_argmax<S>(mv, mi);
+    st_sum<S>(incl);
+    st_argmax<S>(amv, ami);
+    st_argmin<S>(anv, ani);
+  });
+  bcast63(mv, mi);
+  bcast63(amv, ami);
+  bcast63(anv, ani);
   if (mv > c.best_max) {  // strict: PE:608
     c.best_max = mv;
     c.best_idx = mi;
@@ -2134,26 +2286,26 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
     c.kept_slot = c.has_best ? c.best_slot : slot;
     c.kept_iter = c.has_best ? c.best_iter : iter;
     GroupPart kq = q0;
-    if (c.kept_slot != slot) kq = qk(c.kept_slot);
-    double carry = 0.0;
-    {
-      const double sv = lane < ngrp ? kq.sum : 0.0;
-      carry = carry + lane_value(wave_incl_sum(sv), 63);
+    if (c.kept_slot != slot) {  // the speculation missed: the kept slot's chains, plainly
+      kq = qk(c.kept_slot);
+      incl = wave_incl_sum(lane < ngrp ? kq.sum : 0.0);
+      amv = -INFINITY;
+      anv = INFINITY;
+      ami = ani = 0x7fffffff;
+      if (lane < ngrp) {
+        cmb_max(amv, ami, kq.maxw, kq.argmax);
+        cmb_min(anv, ani, kq.minw, kq.argmin);
+      }
+      wave_argmax(amv, ami);
+      wave_argmin(anv, ani);
     }
-    const double S = carry;
+    const double S = 0.0 + lane_value(incl, 63);
     double run = -INFINITY;
-    carry = 0.0;
     {
-      GroupPart q;
-      q.sum = 0.0;
-      q.zmax = -INFINITY;
-      q.zmin = INFINITY;
-      if (lane < ngrp) q = kq;
-      const double incl = wave_incl_sum(q.sum);
       const double prev = wave_shr1(incl, 0.0);
-      const double G = lane == 0 ? carry : carry + prev;
+      const double G = lane == 0 ? 0.0 : 0.0 + prev;
       double cm = -INFINITY;
-      if (lane < ngrp && S != 0.0) cm = (G + (S > 0.0 ? q.zmax : q.zmin)) / S;
+      if (lane < ngrp && S != 0.0) cm = (G + (S > 0.0 ? kq.zmax : kq.zmin)) / S;
       const double im = wave_incl_max(cm);
       double ex = wave_shr1(im, -(double)INFINITY);
       ex = ex > run ? ex : run;
@@ -2163,14 +2315,6 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
       run = tm > run ? tm : run;
     }
     if (S == 0.0) run = -INFINITY;
-    double amv = -INFINITY, anv = INFINITY;
-    int ami = 0x7fffffff, ani = 0x7fffffff;
-    if (lane < ngrp) {
-      cmb_max(amv, ami, kq.maxw, kq.argmax);
-      cmb_min(anv, ani, kq.minw, kq.argmin);
-    }
-    wave_argmax(amv, ami);
-    wave_argmin(anv, ani);
     const double highest = c.has_best ? c.best_max : 0.0;
     c.S = S;
     c.Rmax = run;
@@ -2194,7 +2338,7 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
     SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
     BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart,
     uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
-    double* __restrict__ mlpose, OutDev* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+    double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds wsh;
@@ -2236,14 +2380,10 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
     // block partial (publish_iteration's block level), one arrival
     {
-      const double wd = valid ? (double)w : 0.0;
-      const double wi = wave_incl_sum(wd);
-      const double rmx = wave_max(valid ? wi : -INFINITY);
-      const double rmn = wave_min(valid ? wi : INFINITY);
-      T mx = valid ? w : -inf_t<T>(), mn = valid ? w : inf_t<T>();
-      int ix = valid ? n : 0x7fffffff, in_ = ix;
-      wave_argmax(mx, ix);
-      wave_argmin(mn, in_);
+      double wi, rmx, rmn;
+      T mx, mn;
+      int ix, in_;
+      wave_weight_partials(w, valid, n, wi, rmx, rmn, mx, ix, mn, in_);
       if (lane == 63) wsh.tot[wv] = wi;
       if (lane == 0) {
         wsh.rmax[wv] = rmx;
@@ -2287,41 +2427,48 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
       if (fl.abort) return;
     }
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 2, rt_now());
-    // every block: the group partials (wave w: groups w, w + 4) from all block partials, then the top
-    for (int g = wv; g < fa.ngrp; g += kWaves) {
-      const int b = g * fa.gsz + lane;
-      const bool vb = lane < fa.gsz && b < fa.nblk;
-      double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY, maxw = -INFINITY, minw = INFINITY;
-      int amax = 0x7fffffff, amin = 0x7fffffff;
-      if (vb) {
-        const BlockPart* p = (slot ? part1 : part0) + b;
-        sum = ld_wt_d(&p->sum);
-        maxrel = ld_wt_d(&p->maxrel);
-        minrel = ld_wt_d(&p->minrel);
-        maxw = ld_wt_d(&p->maxw);
-        minw = ld_wt_d(&p->minw);
-        const uint64_t ai = ld_wt(&p->argmax);
-        amax = lo32(ai);
-        amin = hi32(ai);
-      }
-      const GroupPart r = group_math_regs(vb, sum, maxrel, minrel, maxw, minw, amax, amin, b == blk, &fl.bs[slot]);
-      if (lane == 0) fl.gp[slot][g] = r;
+    // every block: the group partials from all block partials, then the top.  Groups are 64 blocks, so
+    // thread t owns blocks t and t + 256 and wave w reduces groups w and w + 4; all six 16-B loads of the
+    // thread are in flight together (one round trip)
+    {
+      const BlockPart* pp = slot ? part1 : part0;
+      const int b0 = threadIdx.x, b1 = threadIdx.x + kBlock;
+      const bool v0 = b0 < fa.nblk, v1 = b1 < fa.nblk;
+      PartRaw r0, r1;
+      ld_part_issue(pp + (v0 ? b0 : 0), r0);
+      ld_part_issue(pp + (v1 ? b1 : 0), r1);
+      wait_parts(r0, r1);
+      if (stamps && threadIdx.x == 0) stamp_max(stamps, 24, rt_now());
+      BlockIn in[2];
+      in[0].vb = v0;
+      in[0].mine = b0 == blk;
+      in[0].p = unpack_part(r0);
+      in[1].vb = v1;
+      in[1].mine = b1 == blk;
+      in[1].p = unpack_part(r1);
+      GroupPart gp[2];
+      group_math2(in, gp, &fl.bs[slot]);
+      if (lane == 0 && wv < fa.ngrp) fl.gp[slot][wv] = gp[0];
+      if (lane == 0 && wv + kWaves < fa.ngrp) fl.gp[slot][wv + kWaves] = gp[1];
     }
+    if (stamps && threadIdx.x == 0) stamp_max(stamps, 25, rt_now());
     __syncthreads();
     if (wv == 0) {
-      GroupPart q0;
-      q0.sum = 0.0;
-      q0.zmax = -INFINITY;
-      q0.zmin = INFINITY;
-      q0.maxw = -INFINITY;
-      q0.minw = INFINITY;
-      q0.argmax = q0.argmin = 0x7fffffff;
-      if (lane < fa.ngrp) q0 = fl.gp[slot][lane];
+      // field-wise LDS reads (an aggregate copy of the conditional struct went through scratch)
       auto qk = [&](int ks) {
-        GroupPart q = q0;
-        if (lane < fa.ngrp) q = fl.gp[ks][lane];
+        const bool v = lane < fa.ngrp;
+        const GroupPart& src = fl.gp[ks][v ? lane : 0];
+        GroupPart q;
+        q.sum = v ? src.sum : 0.0;
+        q.zmax = v ? src.zmax : -INFINITY;
+        q.zmin = v ? src.zmin : INFINITY;
+        q.maxw = v ? src.maxw : -INFINITY;
+        q.minw = v ? src.minw : INFINITY;
+        q.argmax = v ? src.argmax : 0x7fffffff;
+        q.argmin = v ? src.argmin : 0x7fffffff;
         return q;
       };
+      const GroupPart q0 = qk(slot);
       double G = 0.0, Gin = -INFINITY;
       const Ctrl cn = top_math_regs<T, RNG>(fa, c, iter, slot, q0, qk, &G, &Gin);
       if (lane == g_own) {
@@ -2329,6 +2476,7 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
         fl.gs.Gin = Gin;
       }
       if (lane == 0) fl.c = cn;
+      if (stamps && lane == 0) stamp_max(stamps, 26, rt_now());
     }
     __syncthreads();
     c = fl.c;

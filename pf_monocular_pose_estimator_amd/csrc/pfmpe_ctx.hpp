@@ -75,8 +75,9 @@ struct pfmpe_ctx {
   int64_t fused_fallbacks = 0;     // fused frames redone with two launches
   std::map<std::pair<const void*, size_t>, int> occ;  // (kernel, LDS bytes) -> blocks per CU
   Ctrl* d_ctrl = nullptr;
-  OutDev* h_out = nullptr;       // pinned host memory, written by the final wave
-  OutDev* d_out = nullptr;       // its device address
+  RecOut* h_rec = nullptr;       // pinned host memory: the record granules, written by the final wave
+  RecOut* d_out = nullptr;       // its device address
+  OutDev* h_out = nullptr;       // the last record, unpacked on the host by wait_frame
   int32_t seq = 0;               // frame-record sequence number (publication tag = 2 * seq + finished)
   unsigned char* d_table = nullptr;  // this frame's blob table (BlobTable<T> layout)
   unsigned char* h_table = nullptr;  // pinned staging
@@ -174,25 +175,32 @@ inline int harvest_timing(pfmpe_ctx* c) {
   return PFMPE_OK;
 }
 
-// Wait for the frame record: the final block writes it into pinned host memory (then a system-scope
-// fence and the `done` word), so the host spins on that word instead of paying a stream synchronize.
-// The spin is bounded by hipStreamQuery: an idle stream without a record is an error.
+// Wait for the frame record: the final wave writes it into pinned host memory as tagged granules (RecOut),
+// so the host spins on those words instead of paying a stream synchronize, and unpacks them into h_out once
+// every granule carries the tag.  Granule 0 alone with an even tag is an unfinished iteration batch.  The
+// spin is bounded by hipStreamQuery: an idle stream without a record is an error.
+inline bool take_record(pfmpe_ctx* c, int32_t want) {
+  volatile const uint64_t* g = c->h_rec->g;
+  const uint32_t t = (uint32_t)(g[0] >> 32);
+  if ((int32_t)(t >> 1) != want) return false;
+  if (t & 1u) {
+    for (int k = kRecWords - 1; k > 0; --k)
+      if ((uint32_t)(g[k] >> 32) != t) return false;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    uint32_t* w = (uint32_t*)c->h_out;
+    for (int k = 0; k < kRecWords; ++k) w[k] = (uint32_t)g[k];
+  }
+  c->h_out->tag = (int32_t)t;
+  return true;
+}
 inline int wait_frame(pfmpe_ctx* c) {
-  volatile int32_t* tag = &c->h_out->tag;
   const int32_t want = c->seq;
   for (uint64_t spin = 0;; ++spin) {
-    const int32_t t = *tag;
-    if ((t >> 1) == want) {
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // record loads may not move above the tag load
-      return PFMPE_OK;
-    }
+    if (take_record(c, want)) return PFMPE_OK;
     if ((spin & 1023u) == 1023u) {
       const hipError_t q = hipStreamQuery(c->stream);
       if (q == hipSuccess) {
-        if ((*tag >> 1) == want) {
-          __atomic_thread_fence(__ATOMIC_ACQUIRE);
-          return PFMPE_OK;
-        }
+        if (take_record(c, want)) return PFMPE_OK;
         return fail(c, PFMPE_E_HIP, "frame record was not written");
       }
       if (q != hipErrorNotReady) return fail(c, PFMPE_E_HIP, std::string("stream error: ") + hipGetErrorString(q));

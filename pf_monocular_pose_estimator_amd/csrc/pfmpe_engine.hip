@@ -85,7 +85,9 @@ void free_all(pfmpe_ctx* c) {
                  c->d_stamps};
   for (void* p : dev)
     if (p) (void)hipFree(p);
-  if (c->h_out) (void)hipHostFree(c->h_out);
+  if (c->h_rec) (void)hipHostFree(c->h_rec);
+  delete c->h_out;
+  c->h_out = nullptr;
   if (c->h_table) (void)hipHostFree(c->h_table);
   if (c->h_det) (void)hipHostFree(c->h_det);
   for (auto& e : c->ev_pool) {
@@ -170,8 +172,12 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
     ok = ok && hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, c->device) == hipSuccess;
     c->coop = coop != 0;
   }
-  ok &= hipHostMalloc((void**)&c->h_out, sizeof(OutDev), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
-  ok = ok && hipHostGetDevicePointer((void**)&c->d_out, c->h_out, 0) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_rec, sizeof(RecOut), hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+  ok = ok && hipHostGetDevicePointer((void**)&c->d_out, c->h_rec, 0) == hipSuccess;
+  if (ok) {
+    memset(c->h_rec, 0, sizeof(RecOut));
+    c->h_out = new OutDev();
+  }
   ok &= hipMalloc((void**)&c->d_table, table_bytes(c, kMaxBlobs)) == hipSuccess;
   ok &= hipHostMalloc((void**)&c->h_table, table_bytes(c, kMaxBlobs), hipHostMallocDefault) == hipSuccess;
   if (!ok) return bad(PFMPE_E_HIP);
