@@ -2162,32 +2162,38 @@ __global__ __launch_bounds__(kBlock) void k_frame(
 // sits between the weighing pass and the resampling.  Count barrier: one arrival per block; block 0 waits
 // and writes the frame record.  Every wait is bounded (~2 s): an abandoned frame has no record and the
 // host redoes it with two launches.
+struct WaveArg {
+  double maxw, minw;
+  int argmax, argmin;
+};
 struct Frame2Lds {
-  GroupPart gp[2][kFlatMaxGroups];  // group partials per weight slot (the slot's latest iteration)
+  GroupPart gp[2][kFlatMaxGroups];  // group partials per weight slot (sum, zmax, zmin; latest iteration)
+  WaveArg wa[2][kWaves];            // per weight slot: each wave's max / argmax, min / argmin over its blocks
   BlockScan bs[2];                  // this block's in-group scan words per slot
   GroupScan gs;                     // this block's group prefix / running max (kept slot)
   Ctrl c;
   int abort;
 };
 
-// propagate_group's arithmetic for one-tile groups (gsz = 64), TWO groups per wave (the thread's blocks
-// t and t + 256), their chains interleaved; the lane holding block `mine` also returns its scan words
+// propagate_group's sum / running-extrema arithmetic for one-tile groups (gsz = 64), TWO groups per wave
+// (the thread's blocks t and t + 256), their chains interleaved; the lane holding block `mine` also
+// returns its scan words.  The max / argmax and min / argmin go straight over the wave's blocks (wa):
+// the lexicographic (value, index) extremum is exact in any order, so the top combines the four waves'
+// results into exactly the group-then-top answer (a block whose max is NaN drops out either way).
 struct BlockIn {
   bool vb, mine;
   BlockPart p;
 };
-__device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&out)[2], BlockScan* own) {
-  double sum[2], maxrel[2], minrel[2], maxw[2], minw[2];
-  int amax[2], amin[2];
+__device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&out)[2], BlockScan* own, WaveArg& wa) {
+  double sum[2], maxrel[2], minrel[2];
+  double maxw = -INFINITY, minw = INFINITY;
+  int amax = 0x7fffffff, amin = 0x7fffffff;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const bool vb = in[k].vb;
-    maxw[k] = -INFINITY;
-    minw[k] = INFINITY;
-    amax[k] = amin[k] = 0x7fffffff;
     if (vb) {
-      cmb_max(maxw[k], amax[k], in[k].p.maxw, in[k].p.argmax);
-      cmb_min(minw[k], amin[k], in[k].p.minw, in[k].p.argmin);
+      cmb_max(maxw, amax, in[k].p.maxw, in[k].p.argmax);
+      cmb_min(minw, amin, in[k].p.minw, in[k].p.argmin);
     }
     sum[k] = vb ? in[k].p.sum : 0.0;
     maxrel[k] = vb ? in[k].p.maxrel : -INFINITY;
@@ -2198,10 +2204,8 @@ __device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&
     using S = decltype(st);
     st_sum<S>(incl[0]);
     st_sum<S>(incl[1]);
-    st_argmax<S>(maxw[0], amax[0]);
-    st_argmax<S>(maxw[1], amax[1]);
-    st_argmin<S>(minw[0], amin[0]);
-    st_argmin<S>(minw[1], amin[1]);
+    st_argmax<S>(maxw, amax);
+    st_argmin<S>(minw, amin);
   });
   double E[2], zi_max[2], zi_min[2];
 #pragma unroll
@@ -2217,6 +2221,12 @@ __device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&
     st_min<S>(zi_min[0]);
     st_min<S>(zi_min[1]);
   });
+  bcast63(maxw, amax);
+  bcast63(minw, amin);
+  wa.maxw = maxw;
+  wa.minw = minw;
+  wa.argmax = amax;
+  wa.argmin = amin;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     double zp_max = wave_shr1(zi_max[k], -(double)INFINITY), zp_min = wave_shr1(zi_min[k], (double)INFINITY);
@@ -2229,48 +2239,40 @@ __device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&
       own->pad = 0.0;
     }
     const double tmax = lane_value(zi_max[k], 63), tmin = lane_value(zi_min[k], 63);
-    bcast63(maxw[k], amax[k]);
-    bcast63(minw[k], amin[k]);
     GroupPart& r = out[k];
     r.sum = 0.0 + lane_value(incl[k], 63);
     r.zmax = tmax > -INFINITY ? tmax : -INFINITY;
     r.zmin = tmin < INFINITY ? tmin : INFINITY;
-    r.maxw = maxw[k];
-    r.minw = minw[k];
-    r.argmax = amax[k];
-    r.argmin = amin[k];
+    r.maxw = -INFINITY;  // unused on this path (wa)
+    r.minw = INFINITY;
+    r.argmax = r.argmin = 0x7fffffff;
   }
+}
+
+// The 64-lane inclusive sum scan's value on lanes 0-7 when lanes 8-63 hold +0.0: the three in-row steps
+// (the same association), then the one "+ 0.0" the identity steps leave (it only turns -0.0 into +0.0).
+// wave_incl_sum's lane 63 is then 0.0 + this scan's lane 7.
+__device__ __forceinline__ double lanes8_incl_sum(double x) {
+  x = x + dpp<kDppRowShr1>(x, 0.0);
+  x = x + dpp<kDppRowShr2>(x, 0.0);
+  x = x + dpp<kDppRowShr4>(x, 0.0);
+  return x + 0.0;
 }
 
 // propagate_top's one-tile arithmetic (<= 64 groups), partials in registers: q0 = this iteration's partial
 // of the lane's group, qk(slot) = the partial of the lane's group in weight slot `slot` (for the kept
 // slot).  Returns the new control record (wave-uniform) and the lane's group G / Gin when done.
-template <typename T, int RNG, typename KeptF>
+template <typename T, int RNG, typename KeptF, typename ArgF>
 __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, int iter, int slot, const GroupPart& q0,
-                                              KeptF qk, double* G_out, double* Gin_out) {
+                                              KeptF qk, ArgF garg, double* G_out, double* Gin_out) {
   const int lane = lane_id();
   const int ngrp = fa.ngrp;
-  // the exit test's argmax, and speculatively the kept-slot chains for kept slot == this slot (the kept
-  // iteration is an earlier one only when that one holds the best weight): all four interleaved
-  double mv = q0.maxw;
-  int mi = q0.argmax;
-  double incl = lane < ngrp ? q0.sum : 0.0;
-  double amv = -INFINITY, anv = INFINITY;
-  int ami = 0x7fffffff, ani = 0x7fffffff;
-  if (lane < ngrp) {
-    cmb_max(amv, ami, q0.maxw, q0.argmax);
-    cmb_min(anv, ani, q0.minw, q0.argmin);
-  }
-  scan_steps([&](auto st) {
-    using S = decltype(st);
-    st_argmax<S>(mv, mi);
-    st_sum<S>(incl);
-    st_argmax<S>(amv, ami);
-    st_argmin<S>(anv, ani);
-  });
-  bcast63(mv, mi);
-  bcast63(amv, ami);
-  bcast63(anv, ani);
+  // the kept-slot sum chain, speculatively for kept slot == this slot (the kept iteration is an earlier
+  // one only when that one holds the best weight); ngrp <= 8, so the 8-lane form of the scan
+  double incl = lanes8_incl_sum(lane < ngrp ? q0.sum : 0.0);
+  double mv, mn_;
+  int mi, ni_;
+  garg(slot, mv, mi, mn_, ni_);
   if (mv > c.best_max) {  // strict: PE:608
     c.best_max = mv;
     c.best_idx = mi;
@@ -2286,20 +2288,14 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
     c.kept_slot = c.has_best ? c.best_slot : slot;
     c.kept_iter = c.has_best ? c.best_iter : iter;
     GroupPart kq = q0;
-    if (c.kept_slot != slot) {  // the speculation missed: the kept slot's chains, plainly
+    double amv = mv, anv = mn_;
+    int ami = mi, ani = ni_;
+    if (c.kept_slot != slot) {  // the speculation missed: the kept slot's chain
       kq = qk(c.kept_slot);
-      incl = wave_incl_sum(lane < ngrp ? kq.sum : 0.0);
-      amv = -INFINITY;
-      anv = INFINITY;
-      ami = ani = 0x7fffffff;
-      if (lane < ngrp) {
-        cmb_max(amv, ami, kq.maxw, kq.argmax);
-        cmb_min(anv, ani, kq.minw, kq.argmin);
-      }
-      wave_argmax(amv, ami);
-      wave_argmin(anv, ani);
+      incl = lanes8_incl_sum(lane < ngrp ? kq.sum : 0.0);
+      garg(c.kept_slot, amv, ami, anv, ani);
     }
-    const double S = 0.0 + lane_value(incl, 63);
+    const double S = 0.0 + lane_value(incl, 7);
     double run = -INFINITY;
     {
       const double prev = wave_shr1(incl, 0.0);
@@ -2447,7 +2443,9 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
       in[1].mine = b1 == blk;
       in[1].p = unpack_part(r1);
       GroupPart gp[2];
-      group_math2(in, gp, &fl.bs[slot]);
+      WaveArg wa;
+      group_math2(in, gp, &fl.bs[slot], wa);
+      if (lane == 0) fl.wa[slot][wv] = wa;
       if (lane == 0 && wv < fa.ngrp) fl.gp[slot][wv] = gp[0];
       if (lane == 0 && wv + kWaves < fa.ngrp) fl.gp[slot][wv + kWaves] = gp[1];
     }
@@ -2469,8 +2467,20 @@ __global__ __launch_bounds__(kBlock) void k_frame2(
         return q;
       };
       const GroupPart q0 = qk(slot);
+      // the slot's max / argmax, min / argmin: the four waves' results combined (wave-uniform LDS reads)
+      auto garg = [&](int ks, double& mxv, int& mxi, double& mnv, int& mni) {
+        mxv = fl.wa[ks][0].maxw;
+        mxi = fl.wa[ks][0].argmax;
+        mnv = fl.wa[ks][0].minw;
+        mni = fl.wa[ks][0].argmin;
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) {
+          cmb_max(mxv, mxi, fl.wa[ks][w].maxw, fl.wa[ks][w].argmax);
+          cmb_min(mnv, mni, fl.wa[ks][w].minw, fl.wa[ks][w].argmin);
+        }
+      };
       double G = 0.0, Gin = -INFINITY;
-      const Ctrl cn = top_math_regs<T, RNG>(fa, c, iter, slot, q0, qk, &G, &Gin);
+      const Ctrl cn = top_math_regs<T, RNG>(fa, c, iter, slot, q0, qk, garg, &G, &Gin);
       if (lane == g_own) {
         fl.gs.G = G;
         fl.gs.Gin = Gin;
