@@ -11,7 +11,7 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=N, heavy=base.heavy)
     st = syn.make_stream(cfg, 30)
     eng = pf.Engine(0, N); eng.set_model(st.markers, st.K); eng.set_params(pf.default_params()); eng.set_prior(st.prior())
-    eng.set_option(99, 4 | 8)
+    eng.set_option(99, 4 | (8 if fused != 2 else 0))
     eng.set_option(pf.OPT_FUSED, fused)
     rows = []
     for fr in st.frames:
@@ -31,7 +31,7 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
              21: "K2 rows staged (last)", 1: "K1 block partial (last)", 5: "K2 block partial (last)",
              6: "K3 start", 24: "K3 winner reduced / flat partials loaded", 25: "K3 marker minima / flat groups", 26: "K3 pairs / flat top",
              27: "K1 propagated (wave 0, last)", 28: "K1 projected (wave 0, last)", 29: "K1 minima (wave 0, last)",
-             2: "K1 barrier passed (flat, last)", 3: "K1 top done (flat, last)"}
+             2: "K1 barrier passed (flat, last)", 23: "K1 arrival issued (flat, last)", 31: "K1 barrier passed (flat, first)", 3: "K1 top done (flat, last)"}
     raw = np.array(list(s), dtype=np.float64)
     print(f"    candidates visited per particle: mean {raw[30] / N:.1f}  max {raw[31]:.0f}  (last frame, {cfg.M} markers)")
     for i in sorted(names, key=lambda i: r[i]):
