@@ -50,6 +50,7 @@ def parse():
     ap.add_argument("--timing-period", type=int, default=25,
                     help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream)")
     ap.add_argument("--diag", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--prune", type=int, default=1, choices=[0, 1], help="exact blob pruning (1) or brute force (0)")
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
                     "workload; default profiles/pmc_<config>_n<N>.json when present")
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
@@ -76,7 +77,9 @@ def pmc_traffic(path: str, kernel: str):
         return None
     try:
         with open(path) as f:
-            row = json.load(f).get(kernel, {})
+            rows = json.load(f)
+        # PFMPE_K_FRAME times both one-launch shapes; the PMC pass names the kernel itself (k_frame2 by default)
+        row = rows.get(kernel) or (rows.get("k_frame2") if kernel == "k_frame" else None) or {}
         return row.get("hbm_bytes")
     except (OSError, ValueError):
         return None
@@ -144,6 +147,7 @@ def main():
     eng.set_params(prm)
     eng.set_prior(st.prior())
     eng.set_option(pf.OPT_FUSED, args.fused)
+    eng.set_option(pf.OPT_PRUNE, args.prune)
     if args.diag:
         eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])

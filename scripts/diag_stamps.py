@@ -5,7 +5,7 @@ import pf_monocular_pose_estimator_amd as pf
 from pf_monocular_pose_estimator_amd import synthetic as syn
 lib = pf.load()
 lib.pfmpe_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
-fused = int(os.environ.get('PFMPE_FUSED', '1'))
+fused = int(os.environ.get('PFMPE_FUSED', '2'))  # the default frame shape
 for N in [int(x) for x in sys.argv[1:]] or [100000]:
     base = syn.CONFIGS[os.environ.get("PFMPE_CFG", "C2")]
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=N, heavy=base.heavy)
