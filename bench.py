@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--prune", type=int, default=1, choices=[0, 1], help="exact blob pruning (1) or brute force (0)")
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
                     "workload; default profiles/pmc_<config>_n<N>.json when present")
+    ap.add_argument("--keep-prop", type=int, default=1, choices=[0, 1],
+                    help="two-launch path: store the propagated set (1) or regenerate it in k_resample (0)")
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
@@ -148,6 +150,7 @@ def main():
     eng.set_prior(st.prior())
     eng.set_option(pf.OPT_FUSED, args.fused)
     eng.set_option(pf.OPT_PRUNE, args.prune)
+    eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
     if args.diag:
         eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])

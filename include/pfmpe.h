@@ -288,8 +288,13 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *   PFMPE_OPT_FUSED         [2|1|0] run a frame as ONE launch whenever all its blocks fit on the device
  *                                  at once: 2 (default) k_frame2 with flat hand-offs (every block reduces
  *                                  all block partials itself; <= 512 blocks), 1 k_frame with tree
- *                                  hand-offs; 0 forces the two-launch path (k_propagate_weigh + k_resample) */
-enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4 };
+ *                                  hand-offs; 0 forces the two-launch path (k_propagate_weigh + k_resample)
+ *   PFMPE_OPT_KEEP_PROPAGATED [1|0] two-launch path: k_propagate_weigh stores each iteration's propagated
+ *                                  set (two extra state buffers, allocated on first use) and k_resample
+ *                                  gathers from it; 0 regenerates the kept set in k_resample instead.
+ *                                  Results are bit-identical either way */
+enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4,
+       PFMPE_OPT_KEEP_PROPAGATED = 5 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* ----------------------------------------------------------------------- device-resident inputs */

@@ -8,7 +8,7 @@ include/pfmpe.h.  This package holds the in-tree built library (libpfmpe.so), it
 from ._capi import (  # noqa: F401
     Engine, FrameIn, FrameOut, Params, PFError, default_params, load, host_philox, host_ref_uniform,
     STATE_F32, STATE_F64, STATE_F16, RNG_REFERENCE, RNG_PHILOX, FLAG_ACCEPTED, FLAG_REINIT,
-    OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, K_FRAME, K_ROI, K_FINAL, MAX_MARKERS, MAX_BLOBS, LIB_PATH,
+    OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED, K_FRAME, K_ROI, K_FINAL, MAX_MARKERS, MAX_BLOBS, LIB_PATH,
 )
 
 __all__ = [

@@ -20,7 +20,7 @@ OK, E_ARG, E_HIP, E_CAP, E_STATE = 0, -1, -2, -3, -4
 STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
-OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED = 1, 2, 3, 4
+OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED = 1, 2, 3, 4, 5
 K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)

@@ -11,14 +11,16 @@
 //                      group prefixes and the accept test (PE:627-633).  Re-launched only if the exit
 //                      rule did not fire (rare in steady state).
 //   k_resample         stratified resampling (PE:666-682) as a parallel scan + target count per
-//                      particle + wave-cooperative scatter of regenerated particles into the new prior.
+//                      particle + wave-cooperative scatter of the kept particles into the new prior.
 //                      Count partials go up the same 2-level tree; the last group's wave picks the
 //                      winner = argmax count (PE:685-688), computes its pose and pairs and writes the
 //                      frame record straight into pinned host memory.
 //
-// Propagated particles are never written to HBM: they are regenerated from (prior[n], RNG counter)
-// where needed, so the HBM traffic per particle-update is the compulsory 3*S + 8 bytes (S = 48 B for
-// fp32 SoA state; DESIGN.md "Roofline").
+// The one-launch frames (k_frame, k_frame2) keep the propagated particle in registers, so their HBM
+// traffic per particle-update is the compulsory 3*S + 8 bytes (S = 48 B for fp32 SoA state; DESIGN.md
+// "Roofline").  The two-launch path, which is VALU-issue bound at large N, by default stores each
+// iteration's propagated set next to its weights (PFMPE_OPT_KEEP_PROPAGATED; +2*S bytes) and k_resample
+// gathers it, instead of regenerating it (motion model + RNG) from (prior[n], RNG counter).
 //
 // Normalised cumulative weight (DESIGN.md "Exact tiling of the stratified targets"): for particle i of
 // block b in group g,   c_i = fl( fl( G_g + fl( E_b + incl_i ) ) / S )
@@ -1397,7 +1399,8 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
     BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
     GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
-    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, int iter, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, SP* __restrict__ prop0, SP* __restrict__ prop1,
+    int iter, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds sh;
@@ -1427,6 +1430,11 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     int nv = 0;
     w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P, &nv);
     (slot ? w1 : w0)[n] = w;
+    if (prop0) {  // keep the propagated set next to its weights (same slot): k_resample gathers it
+      SP* dst = slot ? prop1 : prop0;
+#pragma unroll
+      for (int q = 0; q < 12; ++q) dst[(int64_t)q * fa.ld + n] = StateIO<T, SP>::store(P[q], fa.anc_out[q]);
+    }
     if (stamps && (fa.diag & 8))  // diagnostic: pruned candidates visited (sum, max)
       atomicAdd((unsigned long long*)(stamps + 30), (unsigned long long)nv), atomicMax((unsigned long long*)(stamps + 31), (unsigned long long)nv);
   }
@@ -1651,7 +1659,7 @@ struct ResampleLds {
 // finishes the frame.  MODE 2 (k_frame2): the same candidate, then a flat arrival on the sharded count
 // counters; block 0 waits for all of them and finishes.  MODE 0 (k_resample) the block only stores its
 // count partial; k_resample_final finishes.
-template <typename T, int RNG, int MAXM, typename SP, int MODE>
+template <typename T, int RNG, int MAXM, typename SP, int MODE, bool RAW = false>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
@@ -1736,7 +1744,10 @@ __device__ __forceinline__ void resample_phase(
     T Q[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) Q[q] = P[q];
-    if (!have_P && !(e > a)) propagate<T, RNG>(fa, sc, A, n, kiter, Q);
+    if (RAW)  // P holds stored state values (fp16: deltas), not the pose: regenerate this one particle
+      make_particle<T, RNG, SP>(fa, sc, prior, n, kiter, Q);
+    else if (!have_P && !(e > a))
+      propagate<T, RNG>(fa, sc, A, n, kiter, Q);
 #pragma unroll
     for (int q = 0; q < 12; ++q) st_wt_d(mlpose + q, (double)Q[q]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drained before the block barrier / arrival
@@ -1770,7 +1781,8 @@ __device__ __forceinline__ void resample_phase(
       if (k < we) {
         const auto& row = rows[own];
 #pragma unroll
-        for (int q = 0; q < 12; ++q) post[(int64_t)q * fa.ld + k] = StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+        for (int q = 0; q < 12; ++q)
+          post[(int64_t)q * fa.ld + k] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
       }
     }
   }
@@ -1784,7 +1796,7 @@ __device__ __forceinline__ void resample_phase(
       for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
       if (lane == 0) cpart[blk] = CountPart{bv, bi};
       const int loc = bi - blk * kBlock;
-      if (lane < 12 && bv > 0) ((T*)(cand + blk))[lane] = sh.rows[loc >> 6][loc & 63].q[lane];
+      if (!RAW && lane < 12 && bv > 0) ((T*)(cand + blk))[lane] = sh.rows[loc >> 6][loc & 63].q[lane];
       if (stamps && lane == 0) stamp_max(stamps, 5, rt_now());
     }
     return;
@@ -1875,7 +1887,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
-    int32_t seq, uint64_t* __restrict__ stamps) {
+    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
@@ -1895,18 +1907,29 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
   const GroupScan gs = gscan[g];
   T A[12];
-  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  if (!prop0 && valid && n >= 2) load_prior(fa, prior, n, A);
   const Ctrl c = *ctrl;
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
+  if (prop0) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
+    const SP* src = c.kept_slot ? prop1 : prop0;
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) A[q] = (T)src[(int64_t)q * fa.ld + n];  // exact (fp16 -> fp32 widening)
+    }
+  }
   stage_consts(fa, sc);  // visible after block_incl_sum's barrier
   const int slot = c.kept_slot;
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
-  resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
-                               mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+  if (prop0)
+    resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
+                                              cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+  else
+    resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
+                                        mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
 }
 
 // ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first
@@ -1917,7 +1940,8 @@ template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
     const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
-    const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+    const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
+    int regen) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the blob table
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
@@ -1979,11 +2003,12 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
   T u0 = (T)0, v0 = (T)0;
   const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
   if (marker_wave) {
-  if (bv > 0) {  // staged by the winner's k_resample block
+  if (bv > 0 && !regen) {  // staged by the winner's k_resample block (regen: k_resample gathered stored
+                           // state values, so the winner's pose is regenerated here)
     const T* row = (const T*)(cand + bi / kBlock);
 #pragma unroll
     for (int q = 0; q < 12; ++q) Pc[q] = row[q];
-  } else {  // every count is 0: the winner is particle 0 (PE:685), never propagated in k_resample
+  } else {  // regen, or every count is 0 (the winner is particle 0, PE:685, never propagated in k_resample)
     make_particle<T, RNG, SP>(fa, sc, prior, bi, c.kept_iter, Pc);
   }
   // wave j: marker j's nearest blob (pose_pairs' scan and tie rule, one marker per wave)
@@ -2328,8 +2353,15 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
   return c;
 }
 
+// The flat frame is one launch only while 2 blocks fit per CU next to the occupancy margin (pfmpe_ctx.hpp
+// frame_fused), i.e. 3 waves per SIMD.  fp64 needs the cap stated (it would take 214 VGPRs, 2 waves, and
+// silently fall back to two launches above 256 blocks); the fp64 TUs define it to 3.  fp32/fp16 fit as they
+// are, and an explicit cap there only trades registers for scratch.
+#ifndef PFMPE_FRAME2_MIN_WAVES
+#define PFMPE_FRAME2_MIN_WAVES 1
+#endif
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) void k_frame2(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_MIN_WAVES))) void k_frame2(
     const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
     SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
     BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart,

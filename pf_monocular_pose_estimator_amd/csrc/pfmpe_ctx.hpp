@@ -47,6 +47,7 @@ struct pfmpe_ctx {
   void* d_state[2] = {nullptr, nullptr};
   int prior_idx = 0;
   void* d_w[2] = {nullptr, nullptr};
+  void* d_prop[2] = {nullptr, nullptr};  // two-launch path: propagated set per weight slot (keep_prop)
   int max_grp = 0;
   BlockPart* d_part[2] = {nullptr, nullptr};
   BlockScan* d_bscan[2] = {nullptr, nullptr};
@@ -101,6 +102,7 @@ struct pfmpe_ctx {
   // options
   bool record_counts = false;
   bool prune = true;
+  bool keep_prop = true;           // PFMPE_OPT_KEEP_PROPAGATED
   int timing = 0;          // HIP-event sampling period in frames (0 = off)
   bool timing_now = false;  // this frame's launches are bracketed
   int64_t timing_frame = 0;
@@ -224,6 +226,15 @@ template <typename T> FrameArgsT<T>& last_args(pfmpe_ctx* c);
 template <> inline FrameArgsT<float>& last_args<float>(pfmpe_ctx* c) { return c->last_fa_f; }
 template <> inline FrameArgsT<double>& last_args<double>(pfmpe_ctx* c) { return c->last_fa_d; }
 
+// the two-launch path's propagated-set buffers (PFMPE_OPT_KEEP_PROPAGATED), allocated on first use: the
+// one-launch frames keep the propagated particle in registers and never need them
+inline int ensure_prop(pfmpe_ctx* c) {
+  if (!c->keep_prop || c->d_prop[0]) return PFMPE_OK;
+  const size_t bytes = (size_t)kPlanes * c->ld * c->es;
+  for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&c->d_prop[i], bytes));
+  return PFMPE_OK;
+}
+
 template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
   static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, int iter) {
@@ -231,17 +242,20 @@ struct Seq {
     const size_t lds = BlobTable<T>::bytes(fa.B);
     uint32_t* gcount = c->d_counters;
     uint32_t* tcount = c->d_counters + c->max_grp;
+    RET(ensure_prop(c));
+    SP* prop0 = c->keep_prop ? (SP*)c->d_prop[0] : nullptr;
+    SP* prop1 = c->keep_prop ? (SP*)c->d_prop[1] : nullptr;
     return launch(c, PFMPE_K_PROPAGATE, [&] {
       if (c->prune)
         hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
                            table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
-                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
-                           c->d_stamps);
+                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, prop0,
+                           prop1, iter, c->d_stamps);
       else
         hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, false, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,
                            table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_bscan[0],
-                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, iter,
-                           c->d_stamps);
+                           c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, gcount, tcount, prop0,
+                           prop1, iter, c->d_stamps);
     });
   }
   static int finish(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
@@ -251,17 +265,19 @@ struct Seq {
     uint32_t* tcount = c->d_counters + 2 * c->max_grp + 1;
     c->seq = (c->seq + 1) & 0x3fffffff;
     const int32_t seq = c->seq;
+    const bool kept = c->keep_prop && c->d_prop[0];  // iterate() allocated them
     RET(launch(c, PFMPE_K_RESAMPLE, [&] {
       hipLaunchKernelGGL((k_resample<T, RNG, MAXM, SP>), dim3(fa.nblk), dim3(kBlock), 0, c->stream, fa, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
-                         c->d_stamps);
+                         c->d_stamps, kept ? (const SP*)c->d_prop[0] : nullptr,
+                         kept ? (const SP*)c->d_prop[1] : nullptr);
     }));
     RET(launch(c, PFMPE_K_FINAL, [&] {
       hipLaunchKernelGGL((k_resample_final<T, RNG, MAXM, SP>), dim3(1), dim3(kFinalBlock), BlobTable<T>::bytes(fa.B),
                          c->stream, fa, c->d_ctrl,
-                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps);
+                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0);
     }));
     RET(wait_frame(c));
     if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed

@@ -79,7 +79,7 @@ void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* 
 
 
 void free_all(pfmpe_ctx* c) {
-  void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_part[0], c->d_part[1],
+  void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
                  c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
@@ -243,6 +243,9 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       return PFMPE_OK;
     case PFMPE_OPT_PRUNE:
       c->prune = value != 0;
+      return PFMPE_OK;
+    case PFMPE_OPT_KEEP_PROPAGATED:
+      c->keep_prop = value != 0;
       return PFMPE_OK;
     case PFMPE_OPT_TIMING:
       if (value < 0 || value > (1 << 20)) return fail(c, PFMPE_E_ARG, "set_option: timing period out of range");

@@ -1,4 +1,5 @@
 // pfmpe_k_f64_philox.hip — kernel instantiations for double state, kRngPhilox (one TU per pair: parallel build).
+#define PFMPE_FRAME2_MIN_WAVES 3  // k_frame2: one launch up to 512 blocks (pf_kernels.hpp)
 #include "pfmpe_ctx.hpp"
 
 namespace pfmpe_impl {

@@ -512,3 +512,40 @@ def test_predict_roi_matches_oracle(state):
                              np.eye(4)[:3].reshape(12), far, syn.IMAGE_W, syn.IMAGE_H, 10)
     assert got["roi"] == roi
     eng.close()
+
+
+@pytest.mark.parametrize("state", ["f64", "f32", "f16"])
+@pytest.mark.parametrize("occlude", [False, True])  # True: one LED hidden -> all 80 iterations, kept slot moves
+def test_kept_propagated_set_is_bit_identical(state, occlude):
+    """Two-launch path: gathering the stored propagated set (PFMPE_OPT_KEEP_PROPAGATED=1, default) and
+    regenerating it in k_resample (=0) give byte-identical frame records and new priors, frame after frame
+    (the stored set follows the weights' slot, so a multi-iteration frame keeps the best iteration's set)."""
+    N, M, B = 3000, 5, 30
+    cfg = syn.StreamConfig("t", M=M, B=B, N=N)
+    st = syn.make_stream(cfg, 3)
+    runs = []
+    for keep in (1, 0):
+        eng = make_engine(N, st.markers, st.K, STATE[state], pf.RNG_PHILOX, fused=0)
+        eng.set_option(pf.OPT_KEEP_PROPAGATED, keep)
+        eng.set_prior(st.prior())
+        recs, priors = [], []
+        for fr in st.frames:
+            blobs = fr.blobs
+            if occlude:
+                true_px = syn.project(st.K, fr.truth, st.markers)
+                outl = np.random.default_rng(fr.index).uniform([0, 0], [syn.IMAGE_W, syn.IMAGE_H], size=(B - M + 1, 2))
+                blobs = np.vstack([true_px[1:], outl])
+            out = eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=blobs, dt=fr.dt,
+                                          seed=11, frame_idx=fr.index)).as_dict()
+            recs.append(out)
+            priors.append(eng.get_particles(1))
+        eng.close()
+        runs.append((recs, priors))
+    (ra, pa), (rb, pb) = runs
+    for oa, ob in zip(ra, rb):
+        for k in oa:
+            assert np.array_equal(np.asarray(oa[k]), np.asarray(ob[k])), k
+    if occlude:
+        assert ra[0]["iters"] > 1 and ra[0]["kept_iter"] >= 0
+    for a, b in zip(pa, pb):
+        assert np.array_equal(a, b)
