@@ -170,11 +170,19 @@ __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
   *s = sin(x);
   *c = cos(x);
 }
-__device__ __forceinline__ float sqrt_t(float x) { return sqrtf(x); }
+// fp32: the hardware square root (v_sqrt_f32, 1 ulp) instead of sqrtf's correctly rounded 14-instruction
+// sequence (tolerance path, like div_t); fp64 stays IEEE
+__device__ __forceinline__ float sqrt_t(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
-// perspective division: fp32 uses one reciprocal, fp64 the exact IEEE quotient (PE:1032)
+// fp32 quotient a/b through the hardware reciprocal (v_rcp_f32, 1 ulp): one instruction instead of the
+// ~10-instruction IEEE division sequence; the fp32 path is a tolerance path, fp64 divides
+// exactly
+__device__ __forceinline__ float rcp_t(float b) { return __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ float div_t(float a, float b) { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ double div_t(double a, double b) { return a / b; }
+// perspective division: fp32 uses one hardware reciprocal, fp64 the exact IEEE quotient (PE:1032)
 __device__ __forceinline__ void persp(float p0, float p1, float p2, float* u, float* v) {
-  const float r = 1.0f / p2;
+  const float r = rcp_t(p2);
   *u = p0 * r;
   *v = p1 * r;
 }
@@ -242,6 +250,13 @@ __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __
 
 // The motion model (PE:543-588) for particle n in PF iteration `iter` from its prior pose A (loaded by
 // load_prior; unused for n < 2); P receives the 3x4 pose.
+template <typename T>
+__device__ __forceinline__ T u21_t(uint32_t v);
+template <>
+__device__ __forceinline__ float u21_t<float>(uint32_t v) { return u21f(v); }
+template <>
+__device__ __forceinline__ double u21_t<double>(uint32_t v) { return u21d(v); }
+
 template <typename T, int RNG>
 __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* A_in, int n,
                                           int iter, T* P) {
@@ -290,7 +305,7 @@ __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsCons
     const T g = (T)gd;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
-      const T u = (T)u21d(r.v[q]);
+      const T u = u21_t<T>(r.v[q]);  // exact in either type
       const T draw = u * (sc.hi[q] - sc.lo[q]) + sc.lo[q];
       d[q] = draw * g;
     }
@@ -522,7 +537,7 @@ __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, c
       if (!(d <= tol_pf)) {
         live = false;  // the reference's break
       } else {
-        const T q = (tol - d) / tol;
+        const T q = div_t(tol - d, tol);
         Pr = Pr + (Mt + q * q);
         bool dup = false;  // an earlier (accepted) pair holds the same blob
 #pragma unroll
