@@ -142,7 +142,10 @@ def main():
     st = syn.make_stream(cfg, n_frames)
     state = args.state or ("f16" if cfg.name == "C4" else "f32")
     state_dtype = {"f32": pf.STATE_F32, "f16": pf.STATE_F16, "f64": pf.STATE_F64}[state]
-    eng = pf.Engine(device=local_rank, max_particles=cfg.N, state_dtype=state_dtype)
+    # one GPU per rank; PFMPE_BENCH_DEVICE pins every rank to one device (rehearsing the multi-rank launch
+    # on a one-GPU box: the ranks then share the card, so the figure is plumbing, not scaling)
+    device = int(os.environ.get("PFMPE_BENCH_DEVICE", local_rank))
+    eng = pf.Engine(device=device, max_particles=cfg.N, state_dtype=state_dtype)
     eng.set_model(st.markers, st.K)
     prm = pf.default_params()
     prm.rng_mode = pf.RNG_PHILOX if args.rng == "philox" else pf.RNG_REFERENCE
