@@ -172,6 +172,11 @@ __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
 }
 // fp32: the hardware square root (v_sqrt_f32, 1 ulp) instead of sqrtf's correctly rounded 14-instruction
 // sequence (tolerance path, like div_t); fp64 stays IEEE
+// max / min for the wave extrema (operands are never NaN: weights are finite, identities are +-inf)
+__device__ __forceinline__ float fmax_t(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ double fmax_t(double a, double b) { return __builtin_fmax(a, b); }
+__device__ __forceinline__ float fmin_t(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ double fmin_t(double a, double b) { return __builtin_fmin(a, b); }
 __device__ __forceinline__ float sqrt_t(float x) { return __builtin_amdgcn_sqrtf(x); }
 __device__ __forceinline__ double sqrt_t(double x) { return sqrt(x); }
 // fp32 quotient a/b through the hardware reciprocal (v_rcp_f32, 1 ulp): one instruction instead of the
@@ -1305,33 +1310,49 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
 }
 
 // A wave's weight partials (the wave-inclusive scan wi of the weights, the extrema of wi over valid lanes,
-// max / argmax and min / argmin of the weights), the independent chains interleaved; the extrema and
-// arg results are wave-uniform
+// max / argmax and min / argmin of the weights); the extrema and arg results are wave-uniform.
+//  * max / min of the weights: value-only DPP reductions (max and min do not round, so any order is exact),
+//    interleaved with the sum scan; argmax / argmin = the first valid lane holding that value (ballot),
+//    i.e. the lowest particle index, exactly the lexicographic (value, index) order of cmb_max / cmb_min.
+//  * extrema of wi: when no valid weight is negative the DPP prefix is non-decreasing over the lanes (each
+//    row_shr / row_bcast step adds a non-negative, lane-monotone addend, and rounding is monotone), so the
+//    maximum is lane 63's total and the minimum lane 0's value (valid lanes are a prefix of the wave).
+//    Only a wave holding a negative weight runs the two prefix max/min scans (wave-uniform branch).
 template <typename T>
 __device__ __forceinline__ void wave_weight_partials(T w, bool valid, int n, double& wi, double& rmx, double& rmn,
                                                      T& mx, int& ix, T& mn, int& in_) {
   wi = valid ? (double)w : 0.0;
   mx = valid ? w : -inf_t<T>();
   mn = valid ? w : inf_t<T>();
-  ix = valid ? n : 0x7fffffff;
-  in_ = ix;
   scan_steps([&](auto st) {
     using S = decltype(st);
     st_sum<S>(wi);
-    st_argmax<S>(mx, ix);
-    st_argmin<S>(mn, in_);
+    mx = fmax_t(mx, dpp<S::ctrl, S::rm>(mx, -inf_t<T>()));
+    mn = fmin_t(mn, dpp<S::ctrl, S::rm>(mn, inf_t<T>()));
   });
-  bcast63(mx, ix);
-  bcast63(mn, in_);
-  rmx = valid ? wi : -INFINITY;
-  rmn = valid ? wi : INFINITY;
-  scan_steps([&](auto st) {
-    using S = decltype(st);
-    st_max<S>(rmx);
-    st_min<S>(rmn);
-  });
-  rmx = lane_value(rmx, 63);
-  rmn = lane_value(rmn, 63);
+  mx = lane_value(mx, 63);
+  mn = lane_value(mn, 63);
+  const uint64_t bx = __ballot(valid && w == mx);
+  const uint64_t bn = __ballot(valid && w == mn);
+  ix = bx ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bx)) : 0x7fffffff;
+  in_ = bn ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bn)) : 0x7fffffff;
+  if (!bx) {  // no valid lane
+    rmx = -INFINITY;
+    rmn = INFINITY;
+  } else if (mn >= (T)0) {
+    rmx = lane_value(wi, 63);
+    rmn = lane_value(wi, 0);
+  } else {
+    rmx = valid ? wi : -INFINITY;
+    rmn = valid ? wi : INFINITY;
+    scan_steps([&](auto st) {
+      using S = decltype(st);
+      st_max<S>(rmx);
+      st_min<S>(rmn);
+    });
+    rmx = lane_value(rmx, 63);
+    rmn = lane_value(rmn, 63);
+  }
 }
 
 // LDS scratch of the per-iteration partials
