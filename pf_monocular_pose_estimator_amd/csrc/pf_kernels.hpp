@@ -1727,7 +1727,18 @@ __device__ __forceinline__ void resample_phase(
     const double cz = (gs.G + zin) / S;
     rin = cz > rin ? cz : rin;
   }
-  const double rm = wave_incl_max(valid ? cn : -INFINITY);
+  // Running max of c over the wave.  With S > 0 and no negative weight in the wave, c is non-decreasing over
+  // its valid lanes (the DPP prefix is lane-monotone, wave_weight_partials; fl(a + x) and x / S > 0 are
+  // monotone in x), so the running max is c itself and the wave's maximum sits in its last valid lane.
+  // Otherwise the fp64 max scan (wave-uniform branch).
+  const uint64_t vmask = __ballot(valid);
+  double rm;
+  if (S > 0.0 && __ballot(valid && wd < 0.0) == 0) {
+    const double last = vmask ? lane_value(cn, 63 - __builtin_clzll(vmask)) : -INFINITY;
+    rm = valid ? cn : last;
+  } else {
+    rm = wave_incl_max(valid ? cn : -INFINITY);
+  }
   if (lane == 63) sh.max[wv] = rm;
   __syncthreads();
   double pm = rin;
