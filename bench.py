@@ -4,9 +4,10 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
 
 N = 1 runs BASELINE.json configs[1] (C2: 5 LEDs, 100k particles, 50 blobs/frame, fp32 state).  For N > 1
-the driver launches one process per GPU with torch.distributed.run; every rank runs an INDEPENDENT camera
-stream (its own seed) on its own GPU — the path shards across streams with no data-path collective
-(SURVEY.md §8e), so scaling is "weak".  gloo (CPU) carries only the barrier and the max-over-ranks time.
+the driver launches one process per GPU with torch.distributed.run and every rank runs configs[4] (C5): an
+INDEPENDENT 1M-particle camera stream (its own seed) on its own GPU — the path shards across streams with no
+data-path collective, so scaling is "weak".  gloo (CPU) carries only the barrier, the
+max-over-ranks time and the sum of updates.
 
 Inputs are resident in HBM before the timed region (pfmpe_stage_blob_bank); each step calls pfmpe_step,
 which is blocking (its last act is the stream synchronize that brings the winner to the host), so the
@@ -39,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C4"])
+    ap.add_argument("--config", default="", choices=["", "C1", "C2", "C3", "C4", "C5"],
+                    help="default: C2 (BASELINE.json configs[1]) at --gpus 1, C5 (configs[4]: one 1M-particle "
+                         "stream per GPU) at --gpus > 1")
     ap.add_argument("--particles", type=int, default=0, help="override N")
     ap.add_argument("--force-iters", type=int, default=0)
     ap.add_argument("--rng", default="philox", choices=["philox", "reference"])
@@ -47,8 +50,18 @@ def parse():
                     help="particle state storage (default: f16 for C4 per BASELINE.json configs[3], else f32)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
-    ap.add_argument("--timing-period", type=int, default=25,
-                    help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream)")
+    ap.add_argument("--timing-period", type=int, default=0,
+                    help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream); "
+                         "default max(1, steps // 10), so at least 10 launches are bracketed")
+    ap.add_argument("--occlude", type=int, default=0, choices=[0, 1],
+                    help="time worst-case frames only: one LED hidden, so the reference's re-draw loop runs all "
+                         "80 iterations (pose_estimator.cpp:535-616)")
+    ap.add_argument("--worst-frames", type=int, default=10,
+                    help="after the timed region, also time this many worst-case (one LED hidden) frames")
+    ap.add_argument("--c1-frames", type=int, default=200, help="C1 oracle frames for the configs[0] CPU baseline")
+    ap.add_argument("--stream-id", type=int, default=-1,
+                    help="camera stream to run (seeds); default = this rank, so rank r runs stream r")
+    ap.add_argument("--dump-records", default="", help=argparse.SUPPRESS)  # tests: per-rank records -> PATH.<rank>.json
     ap.add_argument("--diag", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--prune", type=int, default=1, choices=[0, 1], help="exact blob pruning (1) or brute force (0)")
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
@@ -61,16 +74,32 @@ def parse():
     return ap.parse_args()
 
 
-def algorithmic_bytes(S: int, N: int) -> dict:
-    """Compulsory HBM bytes per launch (DESIGN.md "Roofline")."""
+def algorithmic_bytes(S: int, N: int, k: float = 1.0) -> dict:
+    """Algorithmic HBM bytes per launch, SURVEY.md §8(d)'s canonical figure: 3*S + 8 bytes per particle-update
+    for a k = 1 frame = read prior S + write weight 4 (propagate pass) + read weight 4 + gather-read the kept
+    particle S + write the new prior S (resample pass); every further iteration adds S + 4."""
     return {
-        "k_propagate_weigh": N * (S + 4),      # read prior state, write weight
-        "k_resample": N * (4 + S + S),          # read weight, read prior (regenerate), write new prior
-        "k_frame": N * (S + 4 + S),             # one launch: read prior, write weight, write new prior
-        "k_frame2": N * (S + 4 + S),
-        "k_resample_final": 8 * -(-N // 256),   # read the block count partials
+        "k_propagate_weigh": N * (S + 4),            # one weighing pass: read prior, write weight
+        "k_resample": N * (4 + S + S),               # read weight, gather-read kept particle, write new prior
+        "k_frame": int(N * (k * (S + 4) + 4 + 2 * S)),   # the whole frame in one launch
+        "k_frame2": int(N * (k * (S + 4) + 4 + 2 * S)),
+        "k_resample_final": 8 * -(-N // 256),        # read the block count partials
         "aux": 0,
     }
+
+
+def host_cpu():
+    """CPU model and logical CPU count of this host (the GPU box's host when run there)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return model, os.cpu_count()
 
 
 def pmc_traffic(path: str, kernel: str):
@@ -100,27 +129,61 @@ def combine_ranks(dist, elapsed: float, updates: float):
     return float(t.item()), float(u.item())
 
 
-def cpu_baseline(cfg, n_frames: int):
+def oracle_frames(cfg, n_frames: int, warm: int = 0):
+    """The oracle (single-thread C++ restatement of PE:475-733, the reference's own loop structure with its
+    O(N^2) resampler) over a synthetic stream; per-frame wall time around the PF block only."""
     from oracle import pforacle as orc
     from pf_monocular_pose_estimator_amd import synthetic as syn
-    st = syn.make_stream(cfg, n_frames)
+    st = syn.make_stream(cfg, warm + n_frames)
     prior = st.prior()
     times, iters = [], []
     for fr in st.frames:
         t0 = time.perf_counter()
         out, arr = orc.pf_step(st.markers, st.K, orc.make_params(), prior, fr.current_pose, fr.predicted_pose,
                                fr.prediction, fr.blobs, dt=fr.dt, seed=11 + fr.index, frame_idx=fr.index)
-        times.append(time.perf_counter() - t0)
-        iters.append(out["iters"])
+        if fr.index >= warm:
+            times.append(time.perf_counter() - t0)
+            iters.append(out["iters"])
         if out["resampled"]:
             prior = arr["resampled"]
-    tm = statistics.median(times)
-    k = statistics.median(iters)
-    return {
+    return statistics.median(times), statistics.median(iters)
+
+
+def cpu_baseline(cfg, n_frames: int, c1_frames: int):
+    from pf_monocular_pose_estimator_amd import synthetic as syn
+    model, ncpu = host_cpu()
+    tm, k = oracle_frames(cfg, n_frames)
+    res = {
         "value": cfg.N * k / tm, "unit": "particle-updates/s", "cores": 1, "kind": "port",
         "sample": f"{n_frames} frames of {cfg.name} (N={cfg.N}, M={cfg.M}, B={cfg.B}); oracle/pf_oracle.cpp "
                   f"fp64, median {tm:.3f} s/frame, k={k}; single thread like the reference's ros::spin",
+        "cpu_model": model, "nproc": ncpu,
     }
+    if c1_frames > 0:  # BASELINE.json configs[0]: the reference's own CPU-runnable case
+        c1 = syn.CONFIGS["C1"]
+        t1, k1 = oracle_frames(c1, c1_frames, warm=20)
+        res["c1"] = {"value": c1.N * k1 / t1, "unit": "particle-updates/s", "frames_per_sec": 1.0 / t1,
+                     "ms_per_frame": t1 * 1e3, "iters_per_frame": k1,
+                     "sample": f"C1 (N={c1.N}, M={c1.M}, B={c1.B}): median of {c1_frames} frames after 20 warm-up, "
+                               f"1 thread"}
+    return res
+
+
+def occluded_frames(eng, st, rank: int, n: int, first_index: int):
+    """Worst-case frames: one LED hidden (its blob dropped, an outlier added so B is unchanged), so the
+    maximum weight never reaches M*min(5,B) and the re-draw loop runs all 80 iterations (PE:535-616)."""
+    from pf_monocular_pose_estimator_amd import synthetic as syn
+    frames = []
+    for j in range(n):
+        fr = st.frames[j % len(st.frames)]
+        rng = np.random.default_rng(50_000 + j)
+        true_px = syn.project(st.K, fr.truth, st.markers)
+        near = np.abs(fr.blobs[:, None, :] - true_px[None, 0:1, :]).sum(-1).min(1)
+        keep = fr.blobs[np.argsort(near)[1:]]  # drop the blob closest to LED 0
+        blobs = np.vstack([keep, rng.uniform([0, 0], [syn.IMAGE_W, syn.IMAGE_H], size=(1, 2))])
+        frames.append(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=blobs, dt=fr.dt,
+                                     seed=(rank << 32) + 90_000 + j, frame_idx=first_index + j))
+    return frames
 
 
 def main():
@@ -136,8 +199,10 @@ def main():
     import pf_monocular_pose_estimator_amd as pf
     from pf_monocular_pose_estimator_amd import synthetic as syn
 
-    base = syn.CONFIGS[args.config]
-    cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=args.particles or base.N, heavy=base.heavy, seed=rank)
+    config = args.config or ("C2" if world == 1 else "C5")
+    base = syn.CONFIGS[config]
+    sid = rank if args.stream_id < 0 else args.stream_id
+    cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=args.particles or base.N, heavy=base.heavy, seed=sid)
     n_frames = args.warmup + args.steps
     st = syn.make_stream(cfg, n_frames)
     state = args.state or ("f16" if cfg.name == "C4" else "f32")
@@ -158,14 +223,16 @@ def main():
         eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])
     frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
-                             dt=f.dt, seed=(rank << 32) + 17 + f.index, frame_idx=f.index,
+                             dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index,
                              force_iters=args.force_iters) for f in st.frames]
+    if args.occlude:
+        frames = occluded_frames(eng, st, sid, n_frames, 0)
 
     for i in range(args.warmup):
         eng.step(frames[i])
     eng.reset_kernel_stats()
     if not args.no_timing:
-        eng.set_option(pf.OPT_TIMING, args.timing_period)
+        eng.set_option(pf.OPT_TIMING, args.timing_period or max(1, args.steps // 10))
 
     if dist:
         dist.barrier()
@@ -183,12 +250,35 @@ def main():
     accepted = sum(o.accepted for o in outs)
     stats = eng.kernel_stats()
     eng.set_option(pf.OPT_TIMING, 0)
+    if args.dump_records:  # every timed frame's record + a digest of the final particle set, for the tests
+        import hashlib
+        post = eng.get_particles(1)
+        with open(f"{args.dump_records}.{rank}.json", "w") as f:
+            json.dump({"stream": sid, "records": [{k: np.asarray(v).tolist() for k, v in o.as_dict().items()}
+                                                  for o in outs],
+                       "post_sha1": hashlib.sha1(post.tobytes()).hexdigest()}, f)
+    shape = eng.info(pf.INFO_LAST_SHAPE)
+    fallbacks = eng.info(pf.INFO_FUSED_FALLBACKS)
 
     elapsed, total_updates = combine_ranks(dist, elapsed, updates)
 
+    worst = None
+    if args.worst_frames > 0 and not args.occlude:  # untimed by the driver's contract: reported beside the line
+        wf = occluded_frames(eng, st, sid, args.worst_frames, n_frames)
+        eng.step(wf[0])  # warm the host-blob path
+        t0 = time.perf_counter()
+        wo = eng.step_batch(wf[1:])
+        tw = time.perf_counter() - t0
+        wk = float(np.mean([o.iters for o in wo]))
+        worst = {"what": "one LED hidden: all 80 re-draw iterations (PE:535-616), host-supplied blobs",
+                 "frames": len(wo), "iters_per_frame": wk, "ms_per_frame": tw * 1e3 / len(wo),
+                 "updates_per_s": cfg.N * sum(o.iters for o in wo) / tw,
+                 "accept_rate": sum(o.accepted for o in wo) / len(wo)}
+
     if rank == 0:
         S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
-        ab = algorithmic_bytes(S, cfg.N)
+        k_mean = float(np.mean(iters)) if iters else 1.0
+        ab = algorithmic_bytes(S, cfg.N, k_mean)
         roof = None
         timed = {k: v for k, v in stats.items() if v[0] > 0}
         if timed:
@@ -198,15 +288,21 @@ def main():
             achieved = ab.get(dom, 0) / avg_s / 1e9 if avg_s > 0 else 0.0
             pmc = args.pmc or os.path.join(ROOT, "profiles", f"pmc_{cfg.name.lower()}_n{cfg.N}.json")
             traffic = pmc_traffic(pmc, dom)
+            upd_bytes = 3 * S + 8
+            frame_gbps = total_updates / world / elapsed * upd_bytes / 1e9  # per GPU
             roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                     "traffic": None if traffic is None else round(traffic),
-                    "bytes_per_launch": ab.get(dom, 0), "avg_us": round(avg_s * 1e6, 3),
-                    "per_kernel_avg_us": {k: round(v[1] * 1e3 / v[0], 3) for k, v in timed.items()}}
+                    "traffic_source": os.path.relpath(pmc, ROOT) if traffic is not None else None,
+                    "bytes_per_launch": ab.get(dom, 0), "avg_us": round(avg_s * 1e6, 3), "launches_timed": launches,
+                    "per_kernel_avg_us": {k: round(v[1] * 1e3 / v[0], 3) for k, v in timed.items()},
+                    "frame_level": {"bytes_per_update": upd_bytes, "achieved": round(frame_gbps, 2),
+                                    "frac": round(frame_gbps / HBM_PEAK_GBPS, 4),
+                                    "what": "updates/s per GPU x (3S+8) B (SURVEY.md §8d), whole frame incl. "
+                                            "launch gaps and the host round trip"}}
         cpu = None
         if world == 1 and args.cpu_frames > 0:
-            cpu = cpu_baseline(cfg, args.cpu_frames)
-        k_mean = float(np.mean(iters)) if iters else 0.0
+            cpu = cpu_baseline(cfg, args.cpu_frames, args.c1_frames)
         line = {
             "metric": "particle-updates/sec (propagate+weight+resample) per GPU; frames/sec at N_particles",
             "value": total_updates / elapsed,
@@ -223,7 +319,11 @@ def main():
             "config": {
                 "workload": f"{cfg.name}: {cfg.M} LEDs, {cfg.N} particles, {cfg.B} blobs/frame"
                             f"{' (heavy outliers)' if cfg.heavy else ''}, {state} SoA state"
-                            + (" (BASELINE.json configs[1])" if cfg.name == "C2" else ""),
+                            + {"C2": " (BASELINE.json configs[1])", "C3": " (configs[2])", "C4": " (configs[3])",
+                               "C5": " per GPU (configs[4]: one independent stream per GPU)"}.get(cfg.name, "")
+                            + (", worst case: one LED hidden (80 iterations)" if args.occlude else ""),
+                "frame_shape": {0: "two-launch", 1: "k_frame", 2: "k_frame2"}.get(shape, str(shape)),
+                "fused_fallbacks": fallbacks,
                 "state": state,
                 "N_particles": cfg.N, "markers": cfg.M, "blobs": cfg.B,
                 "frames_per_sec_per_gpu": args.steps / elapsed,
@@ -232,6 +332,7 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "worst_case": worst,
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -292,10 +292,30 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *   PFMPE_OPT_KEEP_PROPAGATED [1|0] two-launch path: k_propagate_weigh stores each iteration's propagated
  *                                  set (two extra state buffers, allocated on first use) and k_resample
  *                                  gathers from it; 0 regenerates the kept set in k_resample instead.
- *                                  Results are bit-identical either way */
+ *                                  Results are bit-identical either way
+ *   PFMPE_OPT_WAIT_BOUND_US [2000000|>=1] bound of every in-launch wait of a one-launch frame.  A frame whose
+ *                                  blocks are not all resident (other work holding CUs) is abandoned at the
+ *                                  bound, redone with two launches (same result) and one-launch frames are
+ *                                  switched off on this context (PFMPE_INFO_FUSED_FALLBACKS counts it;
+ *                                  pfmpe_last_error describes it, the step still returns PFMPE_OK)
+ *   PFMPE_OPT_FUSED_REARM   [0|n]  after such a fallback, switch one-launch frames back on after n clean
+ *                                  two-launch frames (0: stay off)
+ * Within one process at most one one-launch frame runs per device at a time: a context that finds another
+ * context's one-launch frame in flight on its device runs that frame as two launches (PFMPE_INFO_GUARD_SKIPS). */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4,
-       PFMPE_OPT_KEEP_PROPAGATED = 5 };
+       PFMPE_OPT_KEEP_PROPAGATED = 5, PFMPE_OPT_WAIT_BOUND_US = 6, PFMPE_OPT_FUSED_REARM = 7 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
+
+/* Context state for monitoring and tests (no reference counterpart: engine introspection). */
+enum { PFMPE_SHAPE_TWO_LAUNCH = 0, /* k_propagate_weigh (+ re-launches) + k_resample + k_resample_final */
+       PFMPE_SHAPE_FRAME = 1,      /* k_frame: one launch, tree hand-offs                                */
+       PFMPE_SHAPE_FRAME2 = 2 };   /* k_frame2: one launch, flat hand-offs                               */
+enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 after a fallback)       */
+       PFMPE_INFO_FUSED_FALLBACKS = 2,  /* one-launch frames abandoned at the wait bound and redone  */
+       PFMPE_INFO_LAST_SHAPE = 3,       /* PFMPE_SHAPE_* of the last step (-1 before the first)      */
+       PFMPE_INFO_GUARD_SKIPS = 4,      /* frames run as two launches because another was in flight  */
+       PFMPE_INFO_N = 5 };              /* current particle count                                    */
+int pfmpe_get_info(const pfmpe_ctx* ctx, int key, int64_t* value);
 
 /* ----------------------------------------------------------------------- device-resident inputs */
 /* Stages a bank of frames' blob lists in HBM (frame f = blobs[offsets[f] .. offsets[f+1]) rows), so a

@@ -21,6 +21,11 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED = 1, 2, 3, 4, 5
+OPT_WAIT_BOUND_US, OPT_FUSED_REARM = 6, 7
+OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
+DIAG_LAG_LOADS, DIAG_ABANDON = 64, 128
+SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
+INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N = 1, 2, 3, 4, 5
 K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)
@@ -33,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
     "pfmpe_parse_marker_yaml", "pfmpe_default_launch_config", "pfmpe_parse_launch", "pfmpe_parse_camera_info",
     "pfmpe_write_blob_stream", "pfmpe_read_blob_stream", "pfmpe_stage_blob_stream",
-    "pfmpe_default_detect_params", "pfmpe_stage_image", "pfmpe_find_leds",
+    "pfmpe_default_detect_params", "pfmpe_stage_image", "pfmpe_find_leds", "pfmpe_get_info",
 )
 
 
@@ -160,6 +165,7 @@ def load() -> C.CDLL:
         "pfmpe_get_weights": (I, [P, dp]),
         "pfmpe_get_counts": (I, [P, C.POINTER(C.c_uint32)]),
         "pfmpe_set_option": (I, [P, I, I64]),
+        "pfmpe_get_info": (I, [P, I, C.POINTER(I64)]),
         "pfmpe_stage_blob_bank": (I, [P, dp, C.POINTER(C.c_int32), I]),
         "pfmpe_get_kernel_stats": (I, [P, I, C.POINTER(I64), dp]),
         "pfmpe_reset_kernel_stats": (I, [P]),
@@ -252,6 +258,14 @@ class Engine:
 
     def set_option(self, opt: int, value: int):
         self._chk(self.lib.pfmpe_set_option(self.ctx, opt, int(value)))
+
+    def info(self, key: int) -> int:
+        v = C.c_int64()
+        self._chk(self.lib.pfmpe_get_info(self.ctx, key, C.byref(v)))
+        return v.value
+
+    def last_error(self) -> str:
+        return self.lib.pfmpe_last_error(self.ctx).decode()
 
     def set_prior(self, poses: np.ndarray):
         p = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 12)

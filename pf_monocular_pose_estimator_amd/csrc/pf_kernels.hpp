@@ -74,7 +74,8 @@ struct FrameArgsT {
   int32_t N, M, B, it;            // particles, markers, blobs, it_since_initialized_
   int32_t cam_identity, max_iter, force_iters, nblk;
   int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
-  int32_t diag, pad_;             // diagnostic switches (0 in production)
+  int32_t diag;                   // diagnostic switches (0 in production; pfmpe_ctx.hpp kDiag*)
+  uint32_t wait_ticks;            // bound of every in-launch wait, s_memrealtime ticks (100 MHz)
   uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
   int64_t ld;                     // SoA plane stride in elements
   T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
@@ -906,6 +907,15 @@ __device__ __forceinline__ bool wave_arrive_last(uint32_t* counter, int count) {
 // 1/5 last block partial (max), 2-3 / 6-7 top wave start/end, 8 table built, 9 weights done, 10 K2 scan
 // done, 11 counts done, 12 scatter done, 13-18 finalize phases, 19 earliest table built (min).
 constexpr int kStamps = 32;
+// diagnostic switches (FrameArgsT::diag, pfmpe_set_option(ctx, 99, bits)); 0 in production
+enum : int {
+  kDiagStamps = 4,      // phase stamps (s_memrealtime) into d_stamps
+  kDiagVisits = 8,      // pruned-candidate counts into d_stamps
+  kDiagTreeCount = 16,  // k_frame: count barrier as a tree instead of flat
+  kDiagSqrtGroups = 32, // groups of ~sqrt(nblk) blocks even when the frame fits k_frame2
+  kDiagLagLoads = 64,   // k_frame2: the last block sleeps ~20 us before loading the block partials
+  kDiagAbandon = 128    // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
+};
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
 // (min for 0/4/19, max otherwise).  Row 0 holds the single-writer stamps (top / final waves).
@@ -932,7 +942,7 @@ __device__ __forceinline__ void flat_arrive(uint32_t* set, int blk) {  // one la
                          __HIP_MEMORY_SCOPE_AGENT);
 }
 // one wave: poll the set until its shards sum to `target` (true), or give up after ~2 s (false)
-__device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target) {
+__device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target, uint32_t bound) {
   const int lane = lane_id();
   const uint64_t t0 = rt_now();
   for (;;) {
@@ -943,7 +953,7 @@ __device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target) 
 #pragma unroll
     for (int k = 0; k < kShards; ++k) sum += (uint32_t)__builtin_amdgcn_readlane((int)v, k);
     if (sum == target) return true;
-    if (rt_now() - t0 > 200000000ull) return false;  // 2 s at 100 MHz
+    if (rt_now() - t0 > bound) return false;  // PFMPE_OPT_WAIT_BOUND_US (default 2 s)
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -1601,7 +1611,7 @@ __device__ __forceinline__ void finalize_frame(const FrameArgsT<T>& fa, const Ld
       if (lane < kCandGran) gv = ld_wt(&wc->g[lane]);
       const bool stale = lane < kCandGran && (uint32_t)(gv >> 32) != (uint32_t)(tag >> 1);
       if (!__builtin_amdgcn_ballot_w64(stale)) break;
-      if (rt_now() - t0 > 200000000ull) return;  // 2 s: abandon (no record; the host reports it)
+      if (rt_now() - t0 > fa.wait_ticks) return;  // abandon (no record; the host reports it)
       __builtin_amdgcn_s_sleep(1);
     }
     const uint32_t pl = (uint32_t)gv;
@@ -1878,7 +1888,7 @@ __device__ __forceinline__ void resample_phase(
       flat_arrive(flat + kFlatCountSet, blk);
     }
     if (blk != 0) return;
-    if (!flat_wait(flat + kFlatCountSet, fa.flat_base_c + (uint32_t)fa.nblk)) return;  // abandoned: no record
+    if (!flat_wait(flat + kFlatCountSet, fa.flat_base_c + (uint32_t)fa.nblk, fa.wait_ticks)) return;  // abandoned
     int bv = -1, bi = 0x7fffffff;
     for (int t = lane; t < fa.nblk; t += 64) {
       const uint64_t cp = ld_wt(cpart + t);
@@ -2166,7 +2176,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
         const uint64_t t0 = rt_now();
         while (__hip_atomic_load((gu32_t*)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
           __builtin_amdgcn_s_sleep(2);
-          if (rt_now() - t0 > 200000000ull) {  // 2 s at 100 MHz
+          if (rt_now() - t0 > fa.wait_ticks) {  // PFMPE_OPT_WAIT_BOUND_US (default 2 s)
             ab = 1;
             break;
           }
@@ -2484,7 +2494,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
             }
             pre = pre + wsh.tot[ww];
           }
-          BlockPart* bp = (slot ? part1 : part0) + blk;
+          // the partial buffer alternates by ITERATION parity, not by weight slot: an iteration that does
+          // not improve the best weight reuses its slot, and a fast block would then overwrite its partial
+          // while a lagging block still loads the previous iteration's.  Parity is safe: a block stores
+          // iteration i+2's partial (same buffer as i) only after passing iteration i+1's barrier, i.e.
+          // after every block has arrived at i+1, and each block arrives at i+1 only after its iteration-i
+          // loads (wait_parts) have completed.  The per-slot results the frame keeps (group partials,
+          // wave extrema, own scan words) live in LDS.
+          BlockPart* bp = ((iter & 1) ? part1 : part0) + blk;
           st_wt_d(&bp->sum, pre);
           st_wt_d(&bp->maxrel, maxrel);
           st_wt_d(&bp->minrel, minrel);
@@ -2495,7 +2512,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
           flat_arrive(flat, blk);
         }
         const uint32_t target = fa.flat_base_w + (uint32_t)(iter + 1) * (uint32_t)fa.nblk;
-        const bool ok = flat_wait(flat, target);
+        // kDiagAbandon: behave as if the wait bound expired (the host's recovery path under test)
+        const bool ok = !(fa.diag & kDiagAbandon) && flat_wait(flat, target, fa.wait_ticks);
         if (lane == 0 && !ok) fl.abort = 1;
       }
       __syncthreads();
@@ -2506,7 +2524,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     // thread t owns blocks t and t + 256 and wave w reduces groups w and w + 4; all six 16-B loads of the
     // thread are in flight together (one round trip)
     {
-      const BlockPart* pp = slot ? part1 : part0;
+      const BlockPart* pp = (iter & 1) ? part1 : part0;  // iteration parity (see the store above)
+      if ((fa.diag & kDiagLagLoads) && blk == fa.nblk - 1) {  // a lagging reader (the race test)
+        const uint64_t t0 = rt_now();
+        while (rt_now() - t0 < 2000u) __builtin_amdgcn_s_sleep(2);  // ~20 us
+      }
       const int b0 = threadIdx.x, b1 = threadIdx.x + kBlock;
       const bool v0 = b0 < fa.nblk, v1 = b1 < fa.nblk;
       PartRaw r0, r1;

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstddef>
@@ -74,6 +75,12 @@ struct pfmpe_ctx {
   uint32_t* d_flat = nullptr;      // k_frame2 sharded arrival counters (kFlatWords)
   uint32_t flat_base_w = 0, flat_base_c = 0;  // their running totals (host mirror)
   int64_t fused_fallbacks = 0;     // fused frames redone with two launches
+  int fused_user = 2;              // the PFMPE_OPT_FUSED value asked for (fused drops to 0 after a fallback)
+  int64_t fused_rearm = 0;         // PFMPE_OPT_FUSED_REARM: clean two-launch frames before fusing again (0: never)
+  int64_t clean_since_fallback = 0;
+  int64_t wait_bound_us = 2000000; // PFMPE_OPT_WAIT_BOUND_US: bound of every in-launch wait
+  int last_shape = -1;             // PFMPE_SHAPE_* of the last frame
+  int64_t guard_skips = 0;         // one-launch frames run as two launches because another was in flight
   std::map<std::pair<const void*, size_t>, int> occ;  // (kernel, LDS bytes) -> blocks per CU
   Ctrl* d_ctrl = nullptr;
   RecOut* h_rec = nullptr;       // pinned host memory: the record granules, written by the final wave
@@ -126,6 +133,15 @@ struct pfmpe_ctx {
 };
 
 namespace pfmpe_impl {
+
+// One spin-waiting (one-launch) frame per device at a time within this process: two such kernels that each
+// hold part of the CUs could wait on each other until the wait bound abandons a frame.  A context that finds
+// its device busy runs the frame as two launches (they never wait on other blocks, so they always drain).
+constexpr int kMaxDevices = 64;
+inline std::atomic<int>& fused_inflight(int dev) {
+  static std::atomic<int> flags[kMaxDevices];
+  return flags[(dev >= 0 && dev < kMaxDevices) ? dev : 0];
+}
 
 inline int fail(pfmpe_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -304,6 +320,16 @@ struct Seq {
     // "coop-launch"); every in-kernel wait is bounded anyway.
     const int per_cu = std::min(2, it->second - 1);
     if (per_cu < 1 || (int64_t)per_cu * c->num_cu < fa_in.nblk) return PFMPE_OK;  // two-launch path
+    std::atomic<int>& busy = fused_inflight(c->device);
+    int expect = 0;
+    if (!busy.compare_exchange_strong(expect, 1)) {  // another context's one-launch frame is on the device
+      c->guard_skips += 1;
+      return PFMPE_OK;
+    }
+    struct Release {
+      std::atomic<int>& b;
+      ~Release() { b.store(0); }
+    } release{busy};
     FrameArgsT<T> a = fa_in;
     a.flat_base_w = c->flat_base_w;
     a.flat_base_c = c->flat_base_c;
@@ -328,7 +354,7 @@ struct Seq {
                            prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
                            c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
                            tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
-                           c->d_stamps, (c->diag & 16) ? nullptr : c->d_flat);
+                           c->d_stamps, (c->diag & kDiagTreeCount) ? nullptr : c->d_flat);
     }));
     *launched = true;
     if (wait_frame(c) != PFMPE_OK) {
@@ -342,10 +368,15 @@ struct Seq {
       c->flat_base_w = c->flat_base_c = 0;
       c->fused_fallbacks += 1;
       c->fused = 0;
+      c->clean_since_fallback = 0;
+      // not an error (the frame is redone and returns OK); the text and pfmpe_get_info report it
+      c->err = "one-launch frame abandoned at the wait bound (blocks not co-resident: other work on the device?); "
+               "redone with two launches, one-launch frames off" +
+               std::string(c->fused_rearm > 0 ? " until PFMPE_OPT_FUSED_REARM clean frames" : "");
       *launched = false;
       return PFMPE_OK;
     }
-    if (flat || !(c->diag & 16)) {  // the flat counters' new running totals (k_frame: the count set only)
+    if (flat || !(c->diag & kDiagTreeCount)) {  // the flat counters' new running totals (k_frame: the count set only)
       const OutDev& o = *(const OutDev*)c->h_out;
       if (flat) c->flat_base_w += (uint32_t)o.iters * (uint32_t)a.nblk;
       if (o.resampled) c->flat_base_c += (uint32_t)a.nblk;
@@ -355,15 +386,21 @@ struct Seq {
   }
 
   static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
+    if (!c->fused && c->fused_user && c->fused_rearm > 0 && c->clean_since_fallback >= c->fused_rearm)
+      c->fused = c->fused_user;  // re-armed after enough clean two-launch frames
+    const int64_t fallbacks0 = c->fused_fallbacks;
     if (c->fused) {
       bool launched = false;
       RET(c->prune ? frame_fused<true>(c, fa, table, &launched) : frame_fused<false>(c, fa, table, &launched));
       if (launched) {
         if (!frame_done(c)) return fail(c, PFMPE_E_STATE, "fused frame did not finish");
+        c->last_shape = (c->fused == 2 && fa.nblk <= kFlatMaxGroups * kGroup && fa.gsz == kGroup) ? PFMPE_SHAPE_FRAME2
+                                                                                                   : PFMPE_SHAPE_FRAME;
         last_args<T>(c) = fa;
         return PFMPE_OK;
       }
     }
+    c->last_shape = PFMPE_SHAPE_TWO_LAUNCH;
     const int iter_cap = fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter);
     int iter = 0;
     RET(iterate(c, fa, table, iter++));
@@ -377,6 +414,7 @@ struct Seq {
       RET(finish(c, fa, table));
       batch = std::min(batch * 2, 16);
     }
+    if (!c->fused && c->fused_fallbacks == fallbacks0) c->clean_since_fallback += 1;  // not the redone frame
     last_args<T>(c) = fa;
     return PFMPE_OK;
   }
@@ -474,12 +512,13 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   fa.nblk = (c->N + kBlock - 1) / kBlock;
   // groups of 64 whenever the frame can run as one flat launch (k_frame2 reduces one group per wave), so
   // the one-launch and two-launch shapes keep the same summation association; ~sqrt(nblk) beyond
-  fa.gsz = (fa.nblk <= kFlatMaxGroups * kGroup && !(c->diag & 32))
+  fa.gsz = (fa.nblk <= kFlatMaxGroups * kGroup && !(c->diag & kDiagSqrtGroups))
                ? kGroup
                : std::min(kGroup, std::max(1, (int)std::ceil(std::sqrt((double)std::max(1, fa.nblk)))));
   fa.ngrp = (fa.nblk + fa.gsz - 1) / fa.gsz;
   // (c->max_grp = max_blk >= ngrp for every N <= max_particles)
   fa.diag = c->diag;
+  fa.wait_ticks = (uint32_t)std::min<int64_t>(c->wait_bound_us * 100, 0xffffffffll);  // s_memrealtime: 100 MHz
   fa.ld = c->ld;
   return fa;
 }

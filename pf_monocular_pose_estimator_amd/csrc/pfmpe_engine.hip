@@ -239,7 +239,16 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       return PFMPE_OK;
     case PFMPE_OPT_FUSED:
       if (value < 0 || value > 2) return fail(c, PFMPE_E_ARG, "set_option: FUSED is 0, 1 or 2");
-      c->fused = (int)value;
+      c->fused = c->fused_user = (int)value;
+      c->clean_since_fallback = 0;
+      return PFMPE_OK;
+    case PFMPE_OPT_WAIT_BOUND_US:
+      if (value < 1 || value > 40000000) return fail(c, PFMPE_E_ARG, "set_option: WAIT_BOUND_US is 1 .. 4e7");
+      c->wait_bound_us = value;
+      return PFMPE_OK;
+    case PFMPE_OPT_FUSED_REARM:
+      if (value < 0) return fail(c, PFMPE_E_ARG, "set_option: FUSED_REARM >= 0");
+      c->fused_rearm = value;
       return PFMPE_OK;
     case PFMPE_OPT_PRUNE:
       c->prune = value != 0;
@@ -254,7 +263,7 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       return PFMPE_OK;
     case 99:  // undocumented: diagnostic kernel switches for timing experiments
       c->diag = (int)value;
-      if ((c->diag & 4) && !c->d_stamps) {
+      if ((c->diag & kDiagStamps) && !c->d_stamps) {
         RET(set_device(c));
         HIPCHK(c, hipMalloc((void**)&c->d_stamps, (1 + (size_t)c->max_blk) * kStamps * sizeof(uint64_t)));
         HIPCHK(c, hipMemset(c->d_stamps, 0, (1 + (size_t)c->max_blk) * kStamps * sizeof(uint64_t)));
@@ -580,6 +589,18 @@ int pfmpe_get_kernel_stats(pfmpe_ctx* c, int kernel, int64_t* launches, double* 
   if (launches) *launches = c->k_launches[kernel];
   if (total_ms) *total_ms = c->k_ms[kernel];
   return PFMPE_OK;
+}
+
+int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
+  if (!c || !value) return PFMPE_E_ARG;
+  switch (key) {
+    case PFMPE_INFO_FUSED: *value = c->fused; return PFMPE_OK;
+    case PFMPE_INFO_FUSED_FALLBACKS: *value = c->fused_fallbacks; return PFMPE_OK;
+    case PFMPE_INFO_LAST_SHAPE: *value = c->last_shape; return PFMPE_OK;
+    case PFMPE_INFO_GUARD_SKIPS: *value = c->guard_skips; return PFMPE_OK;
+    case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
+    default: return PFMPE_E_ARG;
+  }
 }
 
 int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {

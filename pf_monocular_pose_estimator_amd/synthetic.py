@@ -143,6 +143,9 @@ CONFIGS = {
     "C2": StreamConfig("C2", M=5, B=50, N=100_000),
     "C3": StreamConfig("C3", M=12, B=200, N=1_000_000, heavy=True),
     "C4": StreamConfig("C4", M=5, B=50, N=10_000_000),
+    # BASELINE.json configs[4]: 8 independent camera streams x 1M particles, one stream per GPU (the
+    # per-rank workload of `bench.py --gpus N`; stream seed = rank)
+    "C5": StreamConfig("C5", M=5, B=50, N=1_000_000),
 }
 
 

@@ -250,6 +250,7 @@ def test_fp32_tolerance(rng, N, M, B, heavy):
     prm.rng_mode = RNG[rng]
     eng = make_engine(N, st.markers, st.K, pf.STATE_F32, RNG[rng])
     eng.set_prior(st.prior())
+    compared = 0
     for fr in st.frames:
         prior_used = eng.get_particles(1)  # float-representable values: the oracle starts from the same set
         seed = 50 + fr.index
@@ -276,6 +277,9 @@ def test_fp32_tolerance(rng, N, M, B, heavy):
                 pr, _, _ = orc.optimise_pose(st.markers, st.K, fr.blobs, ref["pairs"], ref["winner_pose"])
                 assert np.abs(pg[[3, 7, 11]] - pr[[3, 7, 11]]).max() < 1e-4
                 assert rotation_angle(syn.to44(pg)[:3, :3], syn.to44(pr)[:3, :3]) < 1e-3
+                compared += 1
+    # the pose criterion must actually have been applied (not vacuously skipped on differing winners)
+    assert compared >= 2, compared
     eng.close()
 
 
