@@ -35,6 +35,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include <hip/hip_fp16.h>
 
 #include "pf_rng.hpp"
@@ -247,11 +249,82 @@ struct StateIO<float, __half> {
   static __device__ __forceinline__ __half store(float v, float anchor) { return __float2half(v - anchor); }
 };
 
+// SoA plane access through a buffer resource (cdna_hip_programming.md T8) for the fp32 / fp16 planes: every
+// plane of particle n is at byte n*sizeof(SP) (one 32-bit VGPR offset shared by all 12 planes) plus the
+// wave-uniform plane offset q*ld*sizeof(SP) in the SGPR soffset, so no plane costs a 64-bit VALU address
+// (a flat access costs two v_mad_u64_u32 and moves per plane).  The resource covers the 12 planes
+// (pfmpe_create caps 12*ld*sizeof(SP) below 4 GiB).  fp64 (the parity mode) keeps flat accesses.
+template <typename SP>
+struct BufPlanes : std::false_type {};
+template <>
+struct BufPlanes<float> : std::true_type {};
+template <>
+struct BufPlanes<__half> : std::true_type {};
+
+template <typename SP>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const SP* base, int64_t ld) {
+  const uint32_t bytes = (uint32_t)(12 * ld * (int64_t)sizeof(SP));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+template <typename SP>
+__device__ __forceinline__ SP buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
+template <>
+__device__ __forceinline__ float buf_ld<float>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+template <>
+__device__ __forceinline__ __half buf_ld<__half>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  return __ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
+}
+__device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_st(__half v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b16(__half_as_ushort(v), r, voff, soff, 0);
+}
+
+// the 12 state values of particle n of a state buffer (raw SP values, no anchor / conversion)
+template <typename SP>
+__device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int64_t ld, int n, SP* v) {
+  if constexpr (BufPlanes<SP>::value) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
+    const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
+#pragma unroll
+    for (int q = 0; q < 12; ++q) v[q] = buf_ld<SP>(r, (uint32_t)n * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) v[q] = base[(int64_t)q * ld + n];
+  }
+}
+// store 12 raw state values as particle k
+template <typename SP>
+__device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t ld, int k, const SP* v) {
+  if constexpr (BufPlanes<SP>::value) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
+    const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
+#pragma unroll
+    for (int q = 0; q < 12; ++q) buf_st(v[q], r, (uint32_t)k * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) base[(int64_t)q * ld + k] = v[q];
+  }
+}
+
 // prior particle n (SoA planes), loaded ahead of use so the loads overlap other work
 template <typename T, typename SP>
 __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __restrict__ prior, int n, T* A) {
+  SP v[12];
+  load_state_raw<SP>(prior, fa.ld, n, v);
 #pragma unroll
-  for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(prior[(int64_t)q * fa.ld + n], fa.anc_in[q]);
+  for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(v[q], fa.anc_in[q]);
+}
+// particle k of a state buffer from its pose P (quantised against the anchor `anc` for fp16 state)
+template <typename T, typename SP>
+__device__ __forceinline__ void store_pose(SP* __restrict__ dst, int64_t ld, int k, const T* P, const T* anc) {
+  SP v[12];
+#pragma unroll
+  for (int q = 0; q < 12; ++q) v[q] = StateIO<T, SP>::store(P[q], anc[q]);
+  store_state_raw<SP>(dst, ld, k, v);
 }
 
 // The motion model (PE:543-588) for particle n in PF iteration `iter` from its prior pose A (loaded by
@@ -442,11 +515,64 @@ struct alignas(2 * sizeof(T)) BlobXY {
 template <typename T>
 struct LdsBlobs;
 
+// bucket_of without branches (fp32 kernels): max(f, 0) maps NaN and negatives to 0 (v_max_f32 returns the
+// non-NaN operand), min(., nb-1) clamps; the same bucket as bucket_of for every input
+__device__ __forceinline__ int bucket_of_bf(float x, float xmin, float inv_bw, int nb) {
+  const float f = (x - xmin) * inv_bw;
+  return (int)__builtin_fminf(__builtin_fmaxf(f, 0.0f), (float)(nb - 1));
+}
+
 template <typename T, int MAXM, bool PRUNE>
 __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u, const T* v,
                                              const LdsBlobs<T>& tb, T* m, int* r) {
   const int B = fa.B, M = fa.M;
   int visited = 0;
+  if constexpr (std::is_same<T, float>::value) {
+    // fp32: branch-free visits on ONE 64-bit key per candidate, {distance bits : original index}.  Distances
+    // are sums of squares (>= +0 or NaN), whose IEEE bits order like the values, and every NaN's bits lie
+    // above +inf's, so "key < best key" is exactly "strictly closer, or equally close with a lower original
+    // index" (the general form's tie rule) and a NaN distance is never taken.  A minimum that stays +inf keeps
+    // r = 0 (the general form's bc < 0 case); it fails the gate anyway.  Candidates go two per step, the
+    // second masked past the window end (its LDS reads stay inside the padded table, kTablePad).
+    // The query buckets: f = (u - (xmin -+ tolq)) * inv_bw, clamped by one med3 (NaN -> bucket 0 or any
+    // in-range bucket: a NaN projection never takes a candidate).  The two roundings of xmin -+ tolq and
+    // u - base are each within half an ulp of a pixel coordinate, like bucket_of's own, far inside tolq's
+    // slack (1e-3 px + 0.1 %): the window still holds every blob within tol_PF.
+    const float fmaxb = (float)(tb.nb - 1);
+    const float base_lo = tb.xmin + fa.tolq, base_hi = tb.xmin - fa.tolq;
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      uint64_t best = ((uint64_t)0x7f800000u << 32) | 0x7fffffffu;
+      if (j < M) {
+        int c0 = 0, c1 = B;
+        if (PRUNE) {
+          const float flo = (u[j] - base_lo) * tb.inv_bw;
+          const float fhi = (u[j] - base_hi) * tb.inv_bw;
+          c0 = tb.bstart[(int)__builtin_amdgcn_fmed3f(flo, 0.0f, fmaxb)];
+          c1 = tb.bstart[(int)__builtin_amdgcn_fmed3f(fhi, 0.0f, fmaxb) + 1];
+        }
+        visited += c1 - c0;
+        const float uj = u[j], vj = v[j];
+        auto visit = [&](BlobXY<float> p, int o, bool in) {
+          const float dx = p.x - uj;
+          const float dy = p.y - vj;
+          const float d = fmadd(dx, dx, dy * dy);
+          const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)o;
+          best = (in & (key < best)) ? key : best;
+        };
+        for (int c = c0; c < c1; c += 2) {
+          const BlobXY<float> pa = tb.bxy[c], pb = tb.bxy[c + 1];
+          const int oa = tb.orig[c], ob = tb.orig[c + 1];
+          visit(pa, oa, true);
+          visit(pb, ob, c + 1 < c1);
+        }
+      }
+      const float bm = __uint_as_float((uint32_t)(best >> 32));
+      m[j] = bm;
+      r[j] = bm < INFINITY ? (int)(uint32_t)best : 0;
+    }
+    return visited;
+  }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     T best = inf_t<T>();
@@ -562,6 +688,36 @@ __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, c
     }
   }
   return Pr;
+}
+
+// The weight of score_minima<PAIRS = false> without the sort, for B >= M (fp32 tolerance path).  With
+// L = min(B, M) = M the cap never binds, and since the extraction runs in ascending distance the reference's
+// break leaves exactly the markers whose own minimum passes the gate: A = {j : sqrt(m_j) <= tol_PF}.  The
+// penalties depend on A only: 3*(1 + ... + D) with D = |A| - #distinct blobs over A (each marker whose blob
+// an earlier marker of A holds, in ANY fixed order, counts once: the same D as in extraction order), and 2
+// per downgraded marker of A.  Only the order of the fp32 additions differs from the extraction order
+// (a few ulp of a weight <= M(M+1)).
+template <int MAXM>
+__device__ __forceinline__ float score_unordered(const FrameArgsT<float>& fa, const float* m, const int* r) {
+  const int M = fa.M;
+  const float tol = fa.tol, tol_pf = fa.tol_pf, Mt = (float)M;
+  const float rtol = rcp_t(tol);
+  float Pr = 0.0f;
+  int dups = 0;
+  bool acc[MAXM];
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    const float d = sqrt_t(m[j]);
+    acc[j] = j < M && d <= tol_pf;
+    const float q = (tol - d) * rtol;
+    Pr = acc[j] ? Pr + (Mt + q * q) : Pr;
+    bool dup = false;
+#pragma unroll
+    for (int e = 0; e < j; ++e) dup |= acc[e] & (r[e] == r[j]);
+    dups += (acc[j] & dup) ? 1 : 0;
+    if ((fa.downgrade >> j) & 1u) Pr = acc[j] ? Pr - 2.0f : Pr;
+  }
+  return Pr - (float)(3 * dups * (dups + 1) / 2);
 }
 
 // ----------------------------------------------------------------------------- wave/block helpers
@@ -914,7 +1070,8 @@ enum : int {
   kDiagTreeCount = 16,  // k_frame: count barrier as a tree instead of flat
   kDiagSqrtGroups = 32, // groups of ~sqrt(nblk) blocks even when the frame fits k_frame2
   kDiagLagLoads = 64,   // k_frame2: the last block sleeps ~20 us before loading the block partials
-  kDiagAbandon = 128    // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
+  kDiagAbandon = 128,   // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
+  kDiagSortedScore = 256  // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -973,6 +1130,9 @@ struct BlobTable {
   static constexpr size_t off_xy(int B) { return off_bstart() + align16((size_t)(bucket_count(B) + 1) * 4); }
   static constexpr size_t off_orig(int B) { return off_xy(B) + align16((size_t)B * sizeof(BlobXY<T>)); }
   static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
+  // LDS of the weighing kernels: the table plus one 16-B granule, so the masked second candidate of the
+  // fp32 column_minima step (index c1 <= B) reads inside the allocation
+  static constexpr size_t lds_bytes(int B) { return bytes(B) + 16; }
 };
 
 template <typename T>
@@ -1314,7 +1474,14 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
     const int visited = column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
     if (nvisit) *nvisit = visited;
     if (st && threadIdx.x == 0) stamp_max(st, 29, rt_now() + (m[0] == (T)12345 ? 1 : 0));
-    w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
+    if constexpr (std::is_same<T, float>::value) {
+      if (fa.B >= fa.M && !(fa.diag & kDiagSortedScore))  // wave-uniform
+        w = score_unordered<MAXM>(fa, m, r);
+      else
+        w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
+    } else {
+      w = score_minima<T, MAXM, false>(fa, m, r, nullptr, nullptr);
+    }
   }
   return w;
 }
@@ -1476,11 +1643,8 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
     int nv = 0;
     w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P, &nv);
     (slot ? w1 : w0)[n] = w;
-    if (prop0) {  // keep the propagated set next to its weights (same slot): k_resample gathers it
-      SP* dst = slot ? prop1 : prop0;
-#pragma unroll
-      for (int q = 0; q < 12; ++q) dst[(int64_t)q * fa.ld + n] = StateIO<T, SP>::store(P[q], fa.anc_out[q]);
-    }
+    if (prop0)  // keep the propagated set next to its weights (same slot): k_resample gathers it
+      store_pose<T, SP>(slot ? prop1 : prop0, fa.ld, n, P, fa.anc_out);
     if (stamps && (fa.diag & 8))  // diagnostic: pruned candidates visited (sum, max)
       atomicAdd((unsigned long long*)(stamps + 30), (unsigned long long)nv), atomicMax((unsigned long long*)(stamps + 31), (unsigned long long)nv);
   }
@@ -1837,9 +2001,10 @@ __device__ __forceinline__ void resample_phase(
       wave_lds_sync();  // rows (before the loop) and this chunk's map reads are done before the next clear
       if (k < we) {
         const auto& row = rows[own];
+        SP v[12];
 #pragma unroll
-        for (int q = 0; q < 12; ++q)
-          post[(int64_t)q * fa.ld + k] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+        for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+        store_state_raw<SP>(post, fa.ld, k, v);
       }
     }
   }
@@ -1972,8 +2137,10 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   if (prop0) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
     const SP* src = c.kept_slot ? prop1 : prop0;
     if (valid) {
+      SP v[12];
+      load_state_raw<SP>(src, fa.ld, n, v);
 #pragma unroll
-      for (int q = 0; q < 12; ++q) A[q] = (T)src[(int64_t)q * fa.ld + n];  // exact (fp16 -> fp32 widening)
+      for (int q = 0; q < 12; ++q) A[q] = (T)v[q];  // exact (fp16 -> fp32 widening)
     }
   }
   stage_consts(fa, sc);  // visible after block_incl_sum's barrier

@@ -255,7 +255,7 @@ template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
   static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, int iter) {
     const SP* prior = (const SP*)c->d_state[c->prior_idx];
-    const size_t lds = BlobTable<T>::bytes(fa.B);
+    const size_t lds = BlobTable<T>::lds_bytes(fa.B);
     uint32_t* gcount = c->d_counters;
     uint32_t* tcount = c->d_counters + c->max_grp;
     RET(ensure_prop(c));
@@ -306,7 +306,7 @@ struct Seq {
     *launched = false;
     const bool flat = c->fused == 2 && fa_in.nblk <= kFlatMaxGroups * kGroup && fa_in.gsz == kGroup && c->d_flat;
     const void* fn = flat ? (const void*)k_frame2<T, RNG, MAXM, PRUNE, SP> : (const void*)k_frame<T, RNG, MAXM, PRUNE, SP>;
-    const size_t lds = BlobTable<T>::bytes(fa_in.B);
+    const size_t lds = BlobTable<T>::lds_bytes(fa_in.B);
     auto key = std::make_pair(fn, lds);
     auto it = c->occ.find(key);
     if (it == c->occ.end()) {

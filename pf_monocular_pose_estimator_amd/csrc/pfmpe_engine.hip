@@ -138,6 +138,12 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   c->ws = state_dtype == PFMPE_STATE_F64 ? 8 : 4;
   c->ld = ((int64_t)max_particles + 63) / 64 * 64;
   c->max_blk = (max_particles + kBlock - 1) / kBlock;
+  // fp32 / fp16 planes are addressed through one 32-bit buffer resource per state buffer
+  // (pf_kernels.hpp BufPlanes): 12 planes must stay below 4 GiB (89M fp32 / 178M fp16 particles)
+  if (state_dtype != PFMPE_STATE_F64 && (int64_t)kPlanes * c->ld * (int64_t)c->es >= ((int64_t)1 << 32)) {
+    delete c;
+    return PFMPE_E_CAP;
+  }
   pfmpe_default_params(&c->params);
   auto bad = [&](int code) {
     free_all(c);
