@@ -69,6 +69,10 @@ def parse():
     ap.add_argument("--keep-prop", type=int, default=1, choices=[0, 1],
                     help="two-launch path: store the propagated set (1) or regenerate it in k_resample (0)")
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
+    ap.add_argument("--multi-sweep", default="",
+                    help="after the timed region, also run S independent streams of the config per GPU as one "
+                         "batch (pfmpe_step_multi) for each S in this comma list; default 1,4,8,16 at C2 on one GPU")
+    ap.add_argument("--multi-steps", type=int, default=50, help="timed batches per multi-stream point")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
     return ap.parse_args()
@@ -186,6 +190,50 @@ def occluded_frames(eng, st, rank: int, n: int, first_index: int):
     return frames
 
 
+def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dtype: int, rng: int, device: int,
+                       sid0: int, prune: int):
+    """S independent streams of `base` on one GPU, each frame of all S run as ONE batch (pfmpe_step_multi:
+    one weighing launch over every stream's blocks, one resampling launch, one finishing launch).  Blob tables
+    come from each stream's staged bank; the loop calls the C-ABI directly (one FFI call per batch)."""
+    import ctypes as C
+    engs, frames = [], []
+    n = warmup + steps
+    try:
+        for s in range(S):
+            cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=1000 * sid0 + s)
+            st = syn.make_stream(cfg, n)
+            eng = pf.Engine(device=device, max_particles=cfg.N, state_dtype=state_dtype)
+            eng.set_model(st.markers, st.K)
+            prm = pf.default_params()
+            prm.rng_mode = rng
+            eng.set_params(prm)
+            eng.set_prior(st.prior())
+            eng.set_option(pf.OPT_PRUNE, prune)
+            eng.stage_blob_bank([f.blobs for f in st.frames])
+            engs.append(eng)
+            frames.append([eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs),
+                                          bank_frame=f.index, dt=f.dt, seed=((1000 * sid0 + s) << 32) + 17 + f.index,
+                                          frame_idx=f.index) for f in st.frames])
+        lib = engs[0].lib
+        ctxs = (C.c_void_p * S)(*[e.ctx.value for e in engs])
+        ins = [(pf.FrameIn * S)(*[frames[s][f] for s in range(S)]) for f in range(n)]
+        outs = [(pf.FrameOut * S)() for _ in range(n)]
+        for f in range(warmup):
+            engs[0]._chk(lib.pfmpe_step_multi(ctxs, S, ins[f], outs[f]))
+        t0 = time.perf_counter()
+        for f in range(warmup, n):
+            engs[0]._chk(lib.pfmpe_step_multi(ctxs, S, ins[f], outs[f]))
+        el = time.perf_counter() - t0
+        upd = sum(base.N * o.iters for f in range(warmup, n) for o in outs[f])
+        acc = sum(o.accepted for f in range(warmup, n) for o in outs[f])
+        return {"streams": S, "N_per_stream": base.N, "live_particles": S * base.N,
+                "updates_per_s": upd / el, "ms_per_batch": el * 1e3 / steps,
+                "frames_per_sec_per_stream": steps / el, "accept_rate": acc / (S * steps)}
+    finally:
+        for e in engs:
+            e.close()
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -275,6 +323,18 @@ def main():
                  "updates_per_s": cfg.N * sum(o.iters for o in wo) / tw,
                  "accept_rate": sum(o.accepted for o in wo) / len(wo)}
 
+    multi = None
+    sweep = args.multi_sweep or ("1,4,8,16" if world == 1 and config == "C2" and not args.occlude else "")
+    if sweep and rank == 0:  # untimed by the driver's contract: reported beside the line
+        Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
+        multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi); "
+                         "frac = updates/s x (3S+8) B / 8 TB/s", "points": []}
+        for S_ in [int(x) for x in sweep.split(",") if x]:
+            pt = multi_stream_point(pf, syn, base, S_, args.multi_steps, 5, state_dtype, prm.rng_mode, device, sid,
+                                    args.prune)
+            pt["frac"] = round(pt["updates_per_s"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
+            multi["points"].append(pt)
+
     if rank == 0:
         S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
         k_mean = float(np.mean(iters)) if iters else 1.0
@@ -333,6 +393,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "worst_case": worst,
+            "multi_stream": multi,
         }
         print(json.dumps(line), flush=True)
     eng.close()

@@ -140,6 +140,16 @@ int pfmpe_step(pfmpe_ctx* ctx, const pfmpe_frame_in* in, pfmpe_frame_out* out);
  * overhead.  Stops at the first error; *done receives the number of frames completed. */
 int pfmpe_step_batch(pfmpe_ctx* ctx, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out, int* done);
 
+/* One frame of each of S independent contexts (camera streams / tracked objects: the reference's
+ * per-object loop, PE:89, with per-object state PE:113-114, 726-727) as ONE batch on the device: the S
+ * weighing passes run as one launch, the S resampling passes as a second, the S frame records as a third
+ * (plus iteration batches for streams whose exit rule does not fire at once).  in[s] / out[s] belong to
+ * ctxs[s]; each context's outputs and state equal what pfmpe_step(ctxs[s], &in[s], &out[s]) gives.
+ * All contexts must be distinct, on one device, of one state type, RNG mode and pruning option; the batch
+ * runs on ctxs[0]'s HIP stream and uses ctxs[0]'s batch scratch.  Blocking.  Errors: PFMPE_E_ARG for a
+ * mismatch (nothing launched), or the failing stream's error text in pfmpe_last_error(ctxs[0]). */
+int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pfmpe_frame_out* out);
+
 /* ---------------------------------------------------------------------- ROI prediction (§8f row 1) */
 /* predictMarkerPositionsInImage (PE:1036-1053) + LEDDetector::determineROI (led_detector.cpp:217-369),
  * as called at PE:396-412: every marker projected through camMoveInv * prior_j * predictionMatrix for all

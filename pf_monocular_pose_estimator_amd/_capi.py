@@ -32,7 +32,7 @@ K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK
 EXPORTED_SYMBOLS = (
     "pfmpe_create", "pfmpe_destroy", "pfmpe_last_error", "pfmpe_abi_version",
     "pfmpe_set_model", "pfmpe_set_params", "pfmpe_default_params", "pfmpe_set_prior",
-    "pfmpe_step", "pfmpe_step_batch", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
+    "pfmpe_step", "pfmpe_step_batch", "pfmpe_step_multi", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
     "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
@@ -161,6 +161,7 @@ def load() -> C.CDLL:
         "pfmpe_set_prior": (I, [P, dp, I]),
         "pfmpe_step": (I, [P, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
         "pfmpe_step_batch": (I, [P, C.POINTER(FrameIn), I, C.POINTER(FrameOut), C.POINTER(I)]),
+        "pfmpe_step_multi": (I, [C.POINTER(P), I, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
         "pfmpe_get_particles": (I, [P, I, dp]),
         "pfmpe_get_weights": (I, [P, dp]),
         "pfmpe_get_counts": (I, [P, C.POINTER(C.c_uint32)]),
@@ -320,6 +321,19 @@ class Engine:
         arr_out = (FrameOut * n)()
         done = C.c_int()
         self._chk(self.lib.pfmpe_step_batch(self.ctx, arr_in, n, arr_out, C.byref(done)))
+        return list(arr_out)
+
+    @staticmethod
+    def step_multi(engines, frames) -> list:
+        """One frame of each engine (independent camera streams / objects) as ONE batch on the device
+        (pfmpe_step_multi): frames[s] belongs to engines[s]; outputs and state equal per-engine step()."""
+        S = len(engines)
+        if S != len(frames) or S == 0:
+            raise ValueError("step_multi: one frame per engine")
+        ctxs = (C.c_void_p * S)(*[e.ctx.value for e in engines])
+        arr_in = (FrameIn * S)(*frames)
+        arr_out = (FrameOut * S)()
+        engines[0]._chk(engines[0].lib.pfmpe_step_multi(ctxs, S, arr_in, arr_out))
         return list(arr_out)
 
     def predict_roi(self, prediction, predicted_pose, D, image_w, image_h, border, cam_move_inv=None) -> dict:

@@ -207,15 +207,18 @@ __device__ __forceinline__ T inf_t() {
 // kernel's first argument, so the block copies them from the kernarg segment with one vector load per
 // lane (no SGPR round trip: kept in SGPRs they spill into VGPR lanes).  Callers barrier afterwards.
 template <typename T>
-__device__ __forceinline__ void stage_consts(const FrameArgsT<T>& fa, LdsConst<T>& sc) {
+__device__ __forceinline__ void stage_consts_from(const uint32_t* src, LdsConst<T>& sc) {
   static_assert(offsetof(FrameArgsT<T>, cur) == 0 && offsetof(FrameArgsT<T>, hi) == offsetof(LdsConst<T>, hi),
                 "LdsConst must mirror the head of FrameArgsT");
   static_assert(sizeof(LdsConst<T>) % 4 == 0, "dword copy");
-  (void)fa;
-  const uint32_t* src = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
   uint32_t* dst = (uint32_t*)&sc;
   constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
   for (int i = threadIdx.x; i < kWordsC; i += kBlock) dst[i] = src[i];
+}
+template <typename T>
+__device__ __forceinline__ void stage_consts(const FrameArgsT<T>& fa, LdsConst<T>& sc) {
+  (void)fa;
+  stage_consts_from<T>((const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), sc);
 }
 
 // ----------------------------------------------------------------------------- pose algebra
@@ -1199,8 +1202,10 @@ inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst
 
 // block-wide copy of the table into LDS (16-byte words); callers barrier before use
 __device__ __forceinline__ void copy_table(const unsigned char* __restrict__ src, unsigned char* dst, size_t bytes) {
-  const uint4* s4 = (const uint4*)src;
-  uint4* d4 = (uint4*)dst;
+  // global loads (src may come from a batched launch's stream descriptor, which hides its address space)
+  typedef __attribute__((address_space(1))) const u32x4_t gv4_t;
+  gv4_t* s4 = (gv4_t*)src;
+  u32x4_t* d4 = (u32x4_t*)dst;
   const int n4 = (int)(bytes / 16);
   for (int i = threadIdx.x; i < n4; i += kBlock) d4[i] = s4[i];
 }
@@ -1213,6 +1218,25 @@ __device__ __forceinline__ Ctrl load_ctrl_wt(const Ctrl* __restrict__ ctrl) {
   uint64_t* d = (uint64_t*)&c;
 #pragma unroll
   for (int q = 0; q < (int)(sizeof(Ctrl) / 8); ++q) d[q] = ld_wt((const uint64_t*)ctrl + q);
+  return c;
+}
+// The control record as written by the previous launch, in scalar registers: the words are read with
+// vector loads (a batched launch reaches the record through a pointer in its stream descriptor, so the
+// compiler cannot use scalar loads) and made wave-uniform with readfirstlane, so every decision on them stays
+// a scalar branch and every buffer resource built from them stays in SGPRs (no waterfall loops).
+__device__ __forceinline__ Ctrl load_ctrl_uniform(const Ctrl* __restrict__ ctrl) {
+  static_assert(sizeof(Ctrl) % 16 == 0, "Ctrl as 16-B words");
+  Ctrl c;
+  const uint4* s = (const uint4*)ctrl;
+  uint32_t* d = (uint32_t*)&c;
+#pragma unroll
+  for (int q = 0; q < (int)(sizeof(Ctrl) / 16); ++q) {
+    const uint4 v = s[q];
+    d[4 * q + 0] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
+    d[4 * q + 1] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.y);
+    d[4 * q + 2] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
+    d[4 * q + 3] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
+  }
   return c;
 }
 __device__ __forceinline__ void store_ctrl_wt(Ctrl* __restrict__ ctrl, const Ctrl& c) {
@@ -1548,7 +1572,8 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
                                                   GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
                                                   Ctrl* __restrict__ ctrl, uint32_t* __restrict__ gcount,
                                                   uint32_t* __restrict__ tcount, uint32_t* __restrict__ gen,
-                                                  uint32_t gen_base, uint64_t* __restrict__ stamps) {
+                                                  uint32_t gen_base, uint64_t* __restrict__ stamps,
+                                                  int blk) {
   // wave partials: scan total, extrema of the wave-inclusive prefix, max/argmax, min/argmin
   double wi, rmx, rmn;
   T mx, mn;
@@ -1567,7 +1592,7 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
   __syncthreads();
   if (wv != 0) return;
 
-  const int g = blockIdx.x / fa.gsz;
+  const int g = blk / fa.gsz;
   const int gsize = min(fa.gsz, fa.nblk - g * fa.gsz);
   int last = 0;
   if (lane == 0) {
@@ -1585,7 +1610,7 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
       }
       pre = pre + sh.tot[ww];
     }
-    BlockPart* bp = (slot ? part1 : part0) + blockIdx.x;
+    BlockPart* bp = (slot ? part1 : part0) + blk;
     st_wt_d(&bp->sum, pre);
     st_wt_d(&bp->maxrel, maxrel);
     st_wt_d(&bp->minrel, minrel);
@@ -1605,31 +1630,31 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
   if (stamps && lane == 0) stamps[3] = rt_now();
 }
 
-// ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread
+// ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread.
+// One block's work (block `blk` of its stream), shared by the one-stream kernel and the batched kernel
+// (k_propagate_weigh_multi, many contexts in one launch).  fa_words: the frame constants' source, the
+// kernarg segment (one-stream) or the stream's descriptor in HBM (batched).
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
-    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior, T* __restrict__ w0,
-    T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
-    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
-    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
-    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, SP* __restrict__ prop0, SP* __restrict__ prop1,
-    int iter, uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ LdsConst<T> sc;
-  __shared__ WeighLds sh;
-
+__device__ __forceinline__ void propagate_weigh_block(
+    const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk, const unsigned char* __restrict__ table,
+    const SP* __restrict__ prior, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
+    BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1,
+    GroupPart* __restrict__ gpart0, GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+    Ctrl* __restrict__ ctrl, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, SP* __restrict__ prop0,
+    SP* __restrict__ prop1, int iter, uint64_t* __restrict__ stamps, unsigned char* smem, LdsConst<T>& sc,
+    WeighLds& sh) {
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
-  const int n = blockIdx.x * kBlock + threadIdx.x;
+  const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < fa.N;
   // table loads first: vmcnt retires in order, so the LDS copy then waits only for them while the
   // prior loads stay in flight across the barrier
   copy_table(table, smem, BlobTable<T>::bytes(fa.B));
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c0 = *ctrl;  // written by the previous launch
+  const Ctrl c0 = load_ctrl_uniform(ctrl);  // written by the previous launch
   if (c0.done) return;    // the exit rule already fired (uniform)
   const int slot = c0.cur_slot;
-  stage_consts(fa, sc);
+  stage_consts_from(fa_words, sc);
   __syncthreads();  // table + constants visible
   const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
   if (stamps && threadIdx.x == 0) {
@@ -1650,7 +1675,76 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   }
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
   publish_iteration<T, RNG>(fa, w, valid, n, slot, iter, sh, part0, part1, bscan0, bscan1, gpart0, gpart1, gscan,
-                            ctrl, gcount, tcount, nullptr, 0u, stamps);
+                            ctrl, gcount, tcount, nullptr, 0u, stamps, blk);
+}
+
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior, T* __restrict__ w0,
+    T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+    uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount, SP* __restrict__ prop0, SP* __restrict__ prop1,
+    int iter, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds sh;
+  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(),
+                                                 (int)blockIdx.x, table, prior, w0, w1, part0, part1, bscan0, bscan1,
+                                                 gpart0, gpart1, gscan, ctrl, gcount, tcount, prop0, prop1, iter,
+                                                 stamps, smem, sc, sh);
+}
+
+// ---- batched frames (pfmpe_step_multi): S independent contexts' frames in one launch.  Each context is one
+// camera stream / tracked object (the reference's per-object loop, PE:89, state per object PE:113-114,
+// 726-727); its blocks are contiguous in the grid.  A stream's descriptor holds its frame constants (the
+// one-stream kernels' kernel arguments) and its device buffers; bmap[block] names the block's stream.
+// Every stream keeps its own hand-off counters, control record and frame record, so the streams of a batch
+// never wait on each other and each one computes exactly what its one-stream frame computes.
+struct Cand;
+template <typename T, typename SP>
+struct StreamDesc {
+  FrameArgsT<T> fa;  // first: stage_consts_from reads its head (LdsConst layout)
+  const unsigned char* table;
+  const SP* prior;
+  SP* post;
+  T* w0;
+  T* w1;
+  BlockPart* part0;
+  BlockPart* part1;
+  BlockScan* bscan0;
+  BlockScan* bscan1;
+  GroupPart* gpart0;
+  GroupPart* gpart1;
+  GroupScan* gscan;
+  Ctrl* ctrl;
+  uint32_t* gcount_w;
+  uint32_t* tcount_w;
+  uint32_t* gcount_r;
+  uint32_t* tcount_r;
+  SP* prop0;  // kept propagated sets (null: k_resample regenerates)
+  SP* prop1;
+  CountPart* cpart;
+  CountPart* cgroup;
+  uint32_t* counts;
+  Cand* cand;
+  double* mlpose;
+  RecOut* out;
+  int32_t seq;
+  int32_t first_blk;  // the stream's first block in the grid
+};
+
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) void k_propagate_weigh_multi(const StreamDesc<T, SP>* __restrict__ descs,
+                                                                  const uint16_t* __restrict__ bmap, int iter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds sh;
+  const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
+  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.table,
+                                                 d.prior, d.w0, d.w1, d.part0, d.part1, d.bscan0, d.bscan1, d.gpart0,
+                                                 d.gpart1, d.gscan, d.ctrl, d.gcount_w, d.tcount_w, d.prop0, d.prop1,
+                                                 iter, nullptr, smem, sc, sh);
 }
 
 // Winner candidate of one block: the block's first max-count particle, its kept pose and its
@@ -1877,10 +1971,10 @@ __device__ __forceinline__ void resample_phase(
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, RecOut* __restrict__ out, int32_t seq,
-    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat = nullptr) {
+    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk) {
   constexpr bool INLAUNCH = MODE != 0;
   const int N = fa.N;
-  const int blk = blockIdx.x, lane = lane_id(), wv = wave_id();
+  const int lane = lane_id(), wv = wave_id();
   const int g = blk / fa.gsz;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < N;
@@ -2101,21 +2195,19 @@ __device__ __forceinline__ void resample_phase(
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
-// ---- launch 2 of the two-launch path: stratified resampling + winner + frame record
+// ---- launch 2 of the two-launch path: stratified resampling + winner + frame record.  One block's work
+// (block `blk` of its stream), shared by k_resample and k_resample_multi.
 template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kBlock) void k_resample(
-    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
-    SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+__device__ __forceinline__ void resample_block(
+    const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk, Ctrl* __restrict__ ctrl,
+    const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post,
+    const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
-    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1) {
-  __shared__ LdsConst<T> sc;
-  __shared__ OutDev rec;
-  __shared__ ResampleLds<T> sh;
-
+    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1,
+    LdsConst<T>& sc, OutDev& rec, ResampleLds<T>& sh) {
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
-  const int blk = blockIdx.x;
   const int g = blk / fa.gsz;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < fa.N;
@@ -2130,7 +2222,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   const GroupScan gs = gscan[g];
   T A[12];
   if (!prop0 && valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c = *ctrl;
+  const Ctrl c = load_ctrl_uniform(ctrl);
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
@@ -2143,17 +2235,47 @@ __global__ __launch_bounds__(kBlock) void k_resample(
       for (int q = 0; q < 12; ++q) A[q] = (T)v[q];  // exact (fp16 -> fp32 widening)
     }
   }
-  stage_consts(fa, sc);  // visible after block_incl_sum's barrier
+  stage_consts_from(fa_words, sc);  // visible after block_incl_sum's barrier
   const int slot = c.kept_slot;
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
   if (prop0)
     resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
-                                              cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+                                              cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps,
+                                              nullptr, blk);
   else
     resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
-                                        mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps);
+                                        mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk);
+}
+
+template <typename T, int RNG, int MAXM, typename SP>
+__global__ __launch_bounds__(kBlock) void k_resample(
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+    const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
+    CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
+    uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
+    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1) {
+  __shared__ LdsConst<T> sc;
+  __shared__ OutDev rec;
+  __shared__ ResampleLds<T> sh;
+  resample_block<T, RNG, MAXM, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
+                                   table, prior, post, w0, w1, bscan0, bscan1, gscan, cpart, cgroup, gcount, tcount,
+                                   counts, cand, mlpose, out, seq, stamps, prop0, prop1, sc, rec, sh);
+}
+
+template <typename T, int RNG, int MAXM, typename SP>
+__global__ __launch_bounds__(kBlock) void k_resample_multi(const StreamDesc<T, SP>* __restrict__ descs,
+                                                           const uint16_t* __restrict__ bmap) {
+  __shared__ LdsConst<T> sc;
+  __shared__ OutDev rec;
+  __shared__ ResampleLds<T> sh;
+  const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
+  resample_block<T, RNG, MAXM, SP>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.ctrl, d.table,
+                                   d.prior, d.post, d.w0, d.w1, d.bscan0, d.bscan1, d.gscan, d.cpart, d.cgroup,
+                                   d.gcount_r, d.tcount_r, d.counts, d.cand, d.mlpose, d.out, d.seq, nullptr, d.prop0,
+                                   d.prop1, sc, rec, sh);
 }
 
 // ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first
@@ -2161,12 +2283,11 @@ __global__ __launch_bounds__(kBlock) void k_resample(
 // reports an unfinished frame (speculative launch) and the re-init branch (PE:707-719).
 constexpr int kFinalBlock = 1024;
 template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kFinalBlock) void k_resample_final(
-    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
+__device__ __forceinline__ void resample_final_block(
+    const FrameArgsT<T>& fa, const uint32_t* fa_words, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
     const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
-    int regen) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];  // the blob table
+    int regen, unsigned char* smem /* the blob table */) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ int sv[kFinalBlock / 64], si[kFinalBlock / 64];
@@ -2178,10 +2299,10 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
   if (stamps && threadIdx.x == 0) stamps[6] = rt_now();
   // nothing below depends on the control record until the reduction is done: the partial, table and
   // most-likely-pose loads go out together with it (on an unfinished frame they are simply unused)
-  const Ctrl c = *ctrl;
+  const Ctrl c = load_ctrl_uniform(ctrl);
   double ml = 0.0;
   if (wv == 0 && lane < 12) ml = mlpose[lane];
-  stage_consts(fa, sc);
+  stage_consts_from(fa_words, sc);
   {
     const uint4* s4 = (const uint4*)table;
     uint4* d4 = (uint4*)smem;
@@ -2274,6 +2395,25 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
   if (stamps && lane == 0) stamps[7] = rt_now();
 }
 
+template <typename T, int RNG, int MAXM, typename SP>
+__global__ __launch_bounds__(kFinalBlock) void k_resample_final(
+    const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
+    const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
+    const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
+    int regen) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  resample_final_block<T, RNG, MAXM, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), ctrl, table, prior,
+                                         cpart, cand, mlpose, out, seq, stamps, regen, smem);
+}
+// batched: block s finishes stream s
+template <typename T, int RNG, int MAXM, typename SP>
+__global__ __launch_bounds__(kFinalBlock) void k_resample_final_multi(const StreamDesc<T, SP>* __restrict__ descs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const StreamDesc<T, SP>& d = descs[blockIdx.x];
+  resample_final_block<T, RNG, MAXM, SP>(d.fa, (const uint32_t*)&d.fa, d.ctrl, d.table, d.prior, d.cpart, d.cand,
+                                         d.mlpose, d.out, d.seq, nullptr, d.prop0 ? 1 : 0, smem);
+}
+
 // ---- the whole frame in ONE cooperative launch (every block co-resident, checked by the host): the
 // PF iterations, the normalisation hand-off and the resampling.  Between the weighing pass and its
 // outcome every block waits for the top wave's release of `gen`; the particle's prior, propagated pose
@@ -2334,7 +2474,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
     }
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
     publish_iteration<T, RNG>(fa, w, valid, n, slot, iter, wsh, part0, part1, bscan0, bscan1, gpart0, gpart1, gscan,
-                              ctrl, gcount_w, tcount_w, gen, gen_base, stamps);
+                              ctrl, gcount_w, tcount_w, gen, gen_base, stamps, blk);
     // wait for this iteration's outcome
     if (wv == 0) {
       int ab = 0;
@@ -2397,10 +2537,11 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   const GroupScan gs = fsh.gs;
   if (flat)  // the count barrier flat (block 0 waits for every arrival), the weighing barrier a tree
     resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
-                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps, flat);
+                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps, flat, blk);
   else
     resample_phase<T, RNG, MAXM, SP, 1>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
-                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps);
+                                        mlpose, cpart, cgroup, gcount_r, tcount_r, counts, out, seq, stamps, nullptr,
+                                        blk);
 }
 
 // ---- the whole frame in ONE launch with FLAT hand-offs (k_frame2; <= 512 co-resident blocks, groups of 64).
@@ -2774,7 +2915,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   const BlockScan bs = fl.bs[kslot];
   const GroupScan gs = fl.gs;
   resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
-                                      mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq, stamps, flat);
+                                      mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq, stamps, flat, blk);
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path).  anchor: the set's

@@ -95,6 +95,11 @@ struct pfmpe_ctx {
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
+  // batch scratch (pfmpe_step_multi, owned by the batch's first context): stream descriptors, the
+  // block -> stream map and host-supplied blob tables, staged in pinned memory and copied in one transfer
+  unsigned char* d_multi = nullptr;
+  unsigned char* h_multi = nullptr;
+  size_t multi_cap = 0;
 
   // model / params
   int M = 0;
@@ -211,12 +216,12 @@ inline bool take_record(pfmpe_ctx* c, int32_t want) {
   c->h_out->tag = (int32_t)t;
   return true;
 }
-inline int wait_frame(pfmpe_ctx* c) {
+inline int wait_frame(pfmpe_ctx* c, hipStream_t on = nullptr) {  // on: the stream the frame runs on
   const int32_t want = c->seq;
   for (uint64_t spin = 0;; ++spin) {
     if (take_record(c, want)) return PFMPE_OK;
     if ((spin & 1023u) == 1023u) {
-      const hipError_t q = hipStreamQuery(c->stream);
+      const hipError_t q = hipStreamQuery(on ? on : c->stream);
       if (q == hipSuccess) {
         if (take_record(c, want)) return PFMPE_OK;
         return fail(c, PFMPE_E_HIP, "frame record was not written");
@@ -418,6 +423,107 @@ struct Seq {
     last_args<T>(c) = fa;
     return PFMPE_OK;
   }
+  // S contexts' frames as ONE batch on cs[0]'s HIP stream (pfmpe_step_multi): one weighing launch over every
+  // stream's blocks, one resampling launch, one finishing launch with a block per stream.  Streams whose exit
+  // rule did not fire on the first iteration get further iteration batches (the others are not relaunched),
+  // exactly as step()'s two-launch path does for one stream.  h / d: the batch scratch, whose first
+  // `tbytes` bytes already hold the host-supplied blob tables; tables[s] are device addresses.
+  static int step_multi(pfmpe_ctx* const* cs, int S, const FrameArgsT<T>* fas, const unsigned char* const* tables,
+                        unsigned char* h, unsigned char* d, size_t tbytes) {
+    using Desc = StreamDesc<T, SP>;
+    pfmpe_ctx* c0 = cs[0];
+    hipStream_t st = c0->stream;
+    for (int s = 0; s < S; ++s) RET(ensure_prop(cs[s]));
+    std::vector<int> act(S);
+    for (int s = 0; s < S; ++s) act[s] = s;
+    const size_t doff = tbytes;
+    int iter = 0, nb = 1;
+    for (int round = 0;; ++round) {
+      const int na = (int)act.size();
+      Desc* hd = (Desc*)(h + doff);
+      const size_t boff = doff + (((size_t)na * sizeof(Desc) + 255) / 256) * 256;
+      uint16_t* hb = (uint16_t*)(h + boff);
+      int64_t total = 0;
+      size_t lds_w = 0, lds_f = 0;
+      for (int i = 0; i < na; ++i) {
+        pfmpe_ctx* c = cs[act[i]];
+        const FrameArgsT<T>& fa = fas[act[i]];
+        Desc& x = hd[i];
+        x.fa = fa;
+        x.table = tables[act[i]];
+        x.prior = (const SP*)c->d_state[c->prior_idx];
+        x.post = (SP*)c->d_state[1 - c->prior_idx];
+        x.w0 = (T*)c->d_w[0];
+        x.w1 = (T*)c->d_w[1];
+        x.part0 = c->d_part[0];
+        x.part1 = c->d_part[1];
+        x.bscan0 = c->d_bscan[0];
+        x.bscan1 = c->d_bscan[1];
+        x.gpart0 = c->d_gpart[0];
+        x.gpart1 = c->d_gpart[1];
+        x.gscan = c->d_gscan;
+        x.ctrl = c->d_ctrl;
+        x.gcount_w = c->d_counters;
+        x.tcount_w = c->d_counters + c->max_grp;
+        x.gcount_r = c->d_counters + c->max_grp + 1;
+        x.tcount_r = c->d_counters + 2 * c->max_grp + 1;
+        const bool kept = c->keep_prop && c->d_prop[0];
+        x.prop0 = kept ? (SP*)c->d_prop[0] : nullptr;
+        x.prop1 = kept ? (SP*)c->d_prop[1] : nullptr;
+        x.cpart = c->d_cpart;
+        x.cgroup = c->d_cgroup;
+        x.counts = c->record_counts ? c->d_counts : nullptr;
+        x.cand = c->d_cand;
+        x.mlpose = c->d_mlpose;
+        x.out = c->d_out;
+        c->seq = (c->seq + 1) & 0x3fffffff;
+        x.seq = c->seq;
+        x.first_blk = (int32_t)total;
+        for (int b = 0; b < fa.nblk; ++b) hb[total + b] = (uint16_t)i;
+        total += fa.nblk;
+        lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.B));
+        lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
+      }
+      const size_t end = boff + (size_t)total * sizeof(uint16_t);
+      const size_t from = round == 0 ? 0 : doff;  // the tables travel with the first round's descriptors
+      HIPCHK(c0, hipMemcpyAsync(d + from, h + from, end - from, hipMemcpyHostToDevice, st));
+      const Desc* dd = (const Desc*)(d + doff);
+      const uint16_t* db = (const uint16_t*)(d + boff);
+      for (int k = 0; k < nb; ++k, ++iter) {
+        if (c0->prune)
+          hipLaunchKernelGGL((k_propagate_weigh_multi<T, RNG, MAXM, true, SP>), dim3((unsigned)total), dim3(kBlock),
+                             lds_w, st, dd, db, iter);
+        else
+          hipLaunchKernelGGL((k_propagate_weigh_multi<T, RNG, MAXM, false, SP>), dim3((unsigned)total), dim3(kBlock),
+                             lds_w, st, dd, db, iter);
+        HIPCHK(c0, hipGetLastError());
+      }
+      hipLaunchKernelGGL((k_resample_multi<T, RNG, MAXM, SP>), dim3((unsigned)total), dim3(kBlock), 0, st, dd, db);
+      HIPCHK(c0, hipGetLastError());
+      hipLaunchKernelGGL((k_resample_final_multi<T, RNG, MAXM, SP>), dim3((unsigned)na), dim3(kFinalBlock), lds_f, st,
+                         dd);
+      HIPCHK(c0, hipGetLastError());
+      std::vector<int> next;
+      for (int i = 0; i < na; ++i) {
+        pfmpe_ctx* c = cs[act[i]];
+        if (wait_frame(c, st) != PFMPE_OK) return fail(c0, PFMPE_E_HIP, "step_multi: stream " + std::to_string(act[i]) + ": " + c->err);
+        if (!frame_done(c)) next.push_back(act[i]);
+      }
+      if (next.empty()) break;
+      for (int s : next) {
+        const FrameArgsT<T>& fa = fas[s];
+        const int cap = fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter);
+        if (iter >= cap) return fail(c0, PFMPE_E_STATE, "step_multi: PF iteration loop did not terminate");
+      }
+      act.swap(next);
+      nb = round == 0 ? 1 : std::min(nb * 2, 16);
+    }
+    for (int s = 0; s < S; ++s) {
+      cs[s]->last_shape = PFMPE_SHAPE_TWO_LAUNCH;
+      last_args<T>(cs[s]) = fas[s];
+    }
+    return PFMPE_OK;
+  }
   static int regen(pfmpe_ctx* c, int kept_iter, const void* prior, double* out) {
     const FrameArgsT<T>& fa = last_args<T>(c);
     return launch(c, PFMPE_K_AUX, [&] {
@@ -443,6 +549,62 @@ int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* tabl
   if (fa.M <= 8) return Seq<T, RNG, 8, SP>::step(c, fa, table);
   if (fa.M <= 12) return Seq<T, RNG, 12, SP>::step(c, fa, table);
   return Seq<T, RNG, 16, SP>::step(c, fa, table);
+}
+
+// pfmpe_step_multi for S validated contexts of one (state type, RNG): frame arguments and blob tables
+// (host-supplied tables staged into the batch scratch of cs[0]), then Seq::step_multi on the marker bucket of
+// the largest M.
+template <typename T, int RNG, typename SP>
+int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
+  pfmpe_ctx* c0 = cs[0];
+  std::vector<FrameArgsT<T>> fas(S);
+  std::vector<size_t> toff(S, 0);
+  size_t tbytes = 0;
+  int64_t total = 0;
+  int maxM = 1;
+  for (int s = 0; s < S; ++s) {
+    pfmpe_ctx* c = cs[s];
+    fas[s] = build_args<T>(c, &in[s]);
+    for (int q = 0; q < 12; ++q) {
+      fas[s].anc_in[q] = (T)c->anchor[c->prior_idx][q];
+      fas[s].anc_out[q] = (T)in[s].current_pose[q];
+    }
+    if (in[s].bank_frame < 0) {
+      toff[s] = tbytes;
+      tbytes += (BlobTable<T>::bytes(in[s].B) + 255) / 256 * 256;
+    }
+    total += fas[s].nblk;
+    maxM = std::max(maxM, c->M);
+  }
+  if (total > 65536 * 256) return fail(c0, PFMPE_E_CAP, "step_multi: too many blocks in one batch");
+  const size_t need = tbytes + ((size_t)S * sizeof(StreamDesc<T, SP>) + 255) / 256 * 256 + (size_t)total * 2 + 256;
+  if (need > c0->multi_cap) {
+    HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    if (c0->d_multi) HIPCHK(c0, hipFree(c0->d_multi));
+    if (c0->h_multi) HIPCHK(c0, hipHostFree(c0->h_multi));
+    c0->d_multi = nullptr;
+    c0->h_multi = nullptr;
+    c0->multi_cap = 0;
+    const size_t cap = std::max(need * 2, (size_t)1 << 16);
+    HIPCHK(c0, hipMalloc((void**)&c0->d_multi, cap));
+    HIPCHK(c0, hipHostMalloc((void**)&c0->h_multi, cap, hipHostMallocDefault));
+    c0->multi_cap = cap;
+  }
+  std::vector<const unsigned char*> tables(S);
+  for (int s = 0; s < S; ++s) {
+    pfmpe_ctx* c = cs[s];
+    if (in[s].bank_frame >= 0) {
+      tables[s] = c->d_bank + c->bank_off[in[s].bank_frame];
+    } else {
+      build_blob_table_host<T>(in[s].blobs, in[s].B, c0->h_multi + toff[s]);
+      tables[s] = c0->d_multi + toff[s];
+    }
+  }
+  if (maxM <= 5) return Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
+  if (maxM <= 8) return Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
+  if (maxM <= 12)
+    return Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
+  return Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
 }
 
 template <typename T, int RNG, typename SP>
@@ -526,6 +688,7 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
 
 #define PFMPE_DECLARE_INSTANCE(T, RNG, SP, EXT)                                                           \
   EXT template int dispatch_m<T, RNG, SP>(pfmpe_ctx*, const pfmpe_frame_in*, const unsigned char*);        \
-  EXT template int regen_m<T, RNG, SP>(pfmpe_ctx*, int, const void*, double*);
+  EXT template int regen_m<T, RNG, SP>(pfmpe_ctx*, int, const void*, double*);                            \
+  EXT template int multi_m<T, RNG, SP>(pfmpe_ctx* const*, int, const pfmpe_frame_in*);
 
 }  // namespace pfmpe_impl

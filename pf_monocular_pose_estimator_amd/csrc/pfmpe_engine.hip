@@ -94,7 +94,57 @@ void free_all(pfmpe_ctx* c) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
+  if (c->d_multi) (void)hipFree(c->d_multi);
+  if (c->h_multi) (void)hipHostFree(c->h_multi);
   if (c->stream) (void)hipStreamDestroy(c->stream);
+}
+
+// pfmpe_step's argument and state checks (also per stream of pfmpe_step_multi)
+int check_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const pfmpe_frame_out* out) {
+  if (!c) return PFMPE_E_ARG;
+  if (!in || !out) return fail(c, PFMPE_E_ARG, "step: null in/out");
+  if (!c->has_model || !c->has_prior) return fail(c, PFMPE_E_STATE, "step: set_model and set_prior first");
+  if (in->B < 0) return fail(c, PFMPE_E_ARG, "step: B < 0");
+  if (in->force_iters < 0 || in->force_iters > kMaxIter) return fail(c, PFMPE_E_ARG, "step: force_iters out of range");
+  if (in->B > c->max_blobs) return fail(c, PFMPE_E_CAP, "step: B exceeds max_blobs");
+  if (in->it_since_init >= 2 && !(in->dt != 0.0))
+    return fail(c, PFMPE_E_ARG, "step: dt must be non-zero in steady state");
+  if (in->bank_frame >= 0) {
+    if (!c->d_bank || in->bank_frame >= (int)c->bank_B.size())
+      return fail(c, PFMPE_E_ARG, "step: bank_frame out of range");
+    if (c->bank_B[in->bank_frame] != in->B) return fail(c, PFMPE_E_ARG, "step: B does not match the staged bank frame");
+  } else if (in->B > 0 && !in->blobs) {
+    return fail(c, PFMPE_E_ARG, "step: null blobs");
+  }
+  return PFMPE_OK;
+}
+
+// the frame record into pfmpe_frame_out, and the context's state after the frame (PE:681, 727)
+void take_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
+  const OutDev& o = *(const OutDev*)c->h_out;
+  out->iters = o.iters;
+  out->kept_iter = o.kept_iter;
+  out->most_likely_idx = o.most_likely_idx;
+  out->accepted = o.accepted;
+  out->resampled = o.resampled;
+  out->winner_idx = o.winner_idx;
+  out->n_corr = o.n_corr;
+  out->flag_fail = o.flag_fail;
+  out->highest_prob = o.highest_prob;
+  out->prob_sum = o.prob_sum;
+  std::memcpy(out->winner_pose, o.winner_pose, sizeof(out->winner_pose));
+  std::memcpy(out->most_likely_pose, o.most_likely_pose, sizeof(out->most_likely_pose));
+  std::memcpy(out->corr, o.corr, sizeof(out->corr));
+
+  c->has_last = true;
+  c->last_prior_idx = c->prior_idx;
+  c->last_accepted = o.resampled != 0;
+  c->last_kept_slot = o.kept_slot;
+  c->last_kept_iter = o.kept_iter;
+  if (o.resampled) {  // newPoseEstimation = resampled set (PE:681, 727), anchored at this frame's current pose
+    c->prior_idx = 1 - c->prior_idx;
+    std::memcpy(c->anchor[c->prior_idx], in->current_pose, 12 * sizeof(double));
+  }
 }
 
 }  // namespace
@@ -339,24 +389,13 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
 }
 
 int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
-  if (!c) return PFMPE_E_ARG;
-  if (!in || !out) return fail(c, PFMPE_E_ARG, "step: null in/out");
-  if (!c->has_model || !c->has_prior) return fail(c, PFMPE_E_STATE, "step: set_model and set_prior first");
-  if (in->B < 0) return fail(c, PFMPE_E_ARG, "step: B < 0");
-  if (in->force_iters < 0 || in->force_iters > kMaxIter) return fail(c, PFMPE_E_ARG, "step: force_iters out of range");
-  if (in->B > c->max_blobs) return fail(c, PFMPE_E_CAP, "step: B exceeds max_blobs");
-  if (in->it_since_init >= 2 && !(in->dt != 0.0))
-    return fail(c, PFMPE_E_ARG, "step: dt must be non-zero in steady state");
+  RET(check_step(c, in, out));
   RET(set_device(c));
   const unsigned char* table = c->d_table;
   const int B = in->B;
   if (in->bank_frame >= 0) {
-    if (!c->d_bank || in->bank_frame >= (int)c->bank_B.size())
-      return fail(c, PFMPE_E_ARG, "step: bank_frame out of range");
-    if (c->bank_B[in->bank_frame] != B) return fail(c, PFMPE_E_ARG, "step: B does not match the staged bank frame");
     table = c->d_bank + c->bank_off[in->bank_frame];
   } else {
-    if (B > 0 && !in->blobs) return fail(c, PFMPE_E_ARG, "step: null blobs");
     // the x-bucketed table is built here, O(B), and travels in the same copy the blobs would
     build_table(c, in->blobs, B, c->h_table);
     HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, table_bytes(c, B), hipMemcpyHostToDevice, c->stream));
@@ -369,31 +408,41 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     c->ev_used = 0;
   }
   RET(rs);
+  take_step(c, in, out);
+  return PFMPE_OK;
+}
 
-  const OutDev& o = *(const OutDev*)c->h_out;
-  out->iters = o.iters;
-  out->kept_iter = o.kept_iter;
-  out->most_likely_idx = o.most_likely_idx;
-  out->accepted = o.accepted;
-  out->resampled = o.resampled;
-  out->winner_idx = o.winner_idx;
-  out->n_corr = o.n_corr;
-  out->flag_fail = o.flag_fail;
-  out->highest_prob = o.highest_prob;
-  out->prob_sum = o.prob_sum;
-  std::memcpy(out->winner_pose, o.winner_pose, sizeof(out->winner_pose));
-  std::memcpy(out->most_likely_pose, o.most_likely_pose, sizeof(out->most_likely_pose));
-  std::memcpy(out->corr, o.corr, sizeof(out->corr));
-
-  c->has_last = true;
-  c->last_prior_idx = c->prior_idx;
-  c->last_accepted = o.resampled != 0;
-  c->last_kept_slot = o.kept_slot;
-  c->last_kept_iter = o.kept_iter;
-  if (o.resampled) {  // newPoseEstimation = resampled set (PE:681, 727), anchored at this frame's current pose
-    c->prior_idx = 1 - c->prior_idx;
-    std::memcpy(c->anchor[c->prior_idx], in->current_pose, 12 * sizeof(double));
+int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
+  if (!ctxs || S < 1 || !ctxs[0]) return PFMPE_E_ARG;
+  pfmpe_ctx* c0 = ctxs[0];
+  if (!in || !out) return fail(c0, PFMPE_E_ARG, "step_multi: null in/out");
+  if (S > 65535) return fail(c0, PFMPE_E_CAP, "step_multi: at most 65535 streams per batch");
+  for (int s = 0; s < S; ++s) {
+    pfmpe_ctx* c = ctxs[s];
+    const std::string who = "step_multi: stream " + std::to_string(s) + ": ";
+    if (!c) return fail(c0, PFMPE_E_ARG, who + "null context");
+    if (c->device != c0->device || c->state_dtype != c0->state_dtype ||
+        c->params.rng_mode != c0->params.rng_mode || c->prune != c0->prune)
+      return fail(c0, PFMPE_E_ARG, who + "device, state type, RNG mode and pruning must match ctxs[0]");
+    for (int e = 0; e < s; ++e)
+      if (ctxs[e] == c) return fail(c0, PFMPE_E_ARG, who + "context appears twice");
+    if (check_step(c, &in[s], &out[s]) != PFMPE_OK) return fail(c0, PFMPE_E_ARG, who + c->err);
   }
+  RET(set_device(c0));
+  const bool ref = c0->params.rng_mode == PFMPE_RNG_REFERENCE;
+  int rs;
+  switch (c0->state_dtype) {
+    case PFMPE_STATE_F64:
+      rs = ref ? multi_m<double, kRngReference, double>(ctxs, S, in) : multi_m<double, kRngPhilox, double>(ctxs, S, in);
+      break;
+    case PFMPE_STATE_F16:
+      rs = ref ? multi_m<float, kRngReference, __half>(ctxs, S, in) : multi_m<float, kRngPhilox, __half>(ctxs, S, in);
+      break;
+    default:
+      rs = ref ? multi_m<float, kRngReference, float>(ctxs, S, in) : multi_m<float, kRngPhilox, float>(ctxs, S, in);
+  }
+  RET(rs);
+  for (int s = 0; s < S; ++s) take_step(ctxs[s], &in[s], &out[s]);
   return PFMPE_OK;
 }
 
