@@ -191,7 +191,7 @@ def occluded_frames(eng, st, rank: int, n: int, first_index: int):
 
 
 def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dtype: int, rng: int, device: int,
-                       sid0: int, prune: int):
+                       sid0: int, prune: int, keep_prop: int):
     """S independent streams of `base` on one GPU, each frame of all S run as ONE batch (pfmpe_step_multi:
     one weighing launch over every stream's blocks, one resampling launch, one finishing launch).  Blob tables
     come from each stream's staged bank; the loop calls the C-ABI directly (one FFI call per batch)."""
@@ -209,6 +209,7 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
             eng.set_params(prm)
             eng.set_prior(st.prior())
             eng.set_option(pf.OPT_PRUNE, prune)
+            eng.set_option(pf.OPT_KEEP_PROPAGATED, keep_prop)
             eng.stage_blob_bank([f.blobs for f in st.frames])
             engs.append(eng)
             frames.append([eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs),
@@ -331,7 +332,7 @@ def main():
                          "frac = updates/s x (3S+8) B / 8 TB/s", "points": []}
         for S_ in [int(x) for x in sweep.split(",") if x]:
             pt = multi_stream_point(pf, syn, base, S_, args.multi_steps, 5, state_dtype, prm.rng_mode, device, sid,
-                                    args.prune)
+                                    args.prune, args.keep_prop)
             pt["frac"] = round(pt["updates_per_s"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
             multi["points"].append(pt)
 

@@ -1220,23 +1220,34 @@ __device__ __forceinline__ Ctrl load_ctrl_wt(const Ctrl* __restrict__ ctrl) {
   for (int q = 0; q < (int)(sizeof(Ctrl) / 8); ++q) d[q] = ld_wt((const uint64_t*)ctrl + q);
   return c;
 }
-// The control record as written by the previous launch, in scalar registers: the words are read with
-// vector loads (a batched launch reaches the record through a pointer in its stream descriptor, so the
-// compiler cannot use scalar loads) and made wave-uniform with readfirstlane, so every decision on them stays
-// a scalar branch and every buffer resource built from them stays in SGPRs (no waterfall loops).
+// The control record as written by the previous launch, in scalar registers, by scalar loads: the address is
+// wave-uniform (a kernel argument, or read from a batched launch's stream descriptor, where the compiler would
+// otherwise issue vector loads that wait behind the block's earlier vector loads in vmcnt order).  Scalar
+// loads are safe here: the record was written by an earlier launch (the scalar cache starts each dispatch
+// invalidated) and this launch writes it only after every read.  Decisions on it stay scalar branches and
+// buffer resources built from it stay in SGPRs (no waterfall loops).
+typedef uint32_t u32x16_t __attribute__((ext_vector_type(16)));
+// one dword of the control record by a scalar load (same conditions as load_ctrl_uniform)
+template <int OFF>
+__device__ __forceinline__ int load_ctrl_word(const Ctrl* __restrict__ ctrl) {
+  int v;
+  asm volatile("s_load_dword %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(ctrl), "i"(OFF) : "memory");
+  return v;
+}
 __device__ __forceinline__ Ctrl load_ctrl_uniform(const Ctrl* __restrict__ ctrl) {
-  static_assert(sizeof(Ctrl) % 16 == 0, "Ctrl as 16-B words");
+  static_assert(sizeof(Ctrl) == 80, "Ctrl = 16 + 4 dwords");
+  u32x16_t a;
+  u32x4_t b;
+  asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+               : "=s"(a), "=s"(b)
+               : "s"(ctrl)
+               : "memory");
   Ctrl c;
-  const uint4* s = (const uint4*)ctrl;
   uint32_t* d = (uint32_t*)&c;
 #pragma unroll
-  for (int q = 0; q < (int)(sizeof(Ctrl) / 16); ++q) {
-    const uint4 v = s[q];
-    d[4 * q + 0] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
-    d[4 * q + 1] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.y);
-    d[4 * q + 2] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
-    d[4 * q + 3] = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
-  }
+  for (int q = 0; q < 16; ++q) d[q] = a[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) d[16 + q] = b[q];
   return c;
 }
 __device__ __forceinline__ void store_ctrl_wt(Ctrl* __restrict__ ctrl, const Ctrl& c) {
@@ -1634,7 +1645,7 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
 // One block's work (block `blk` of its stream), shared by the one-stream kernel and the batched kernel
 // (k_propagate_weigh_multi, many contexts in one launch).  fa_words: the frame constants' source, the
 // kernarg segment (one-stream) or the stream's descriptor in HBM (batched).
-template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP, bool MULTI>
 __device__ __forceinline__ void propagate_weigh_block(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
@@ -1651,9 +1662,10 @@ __device__ __forceinline__ void propagate_weigh_block(
   copy_table(table, smem, BlobTable<T>::bytes(fa.B));
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c0 = load_ctrl_uniform(ctrl);  // written by the previous launch
-  if (c0.done) return;    // the exit rule already fired (uniform)
-  const int slot = c0.cur_slot;
+  // written by the previous launch: the exit rule already fired (uniform), and this iteration's weight slot
+  // (a kernel argument pointer: the compiler's own scalar loads; batched: explicit scalar loads)
+  if (MULTI ? load_ctrl_word<(int)offsetof(Ctrl, done)>(ctrl) : ctrl->done) return;
+  const int slot = MULTI ? load_ctrl_word<(int)offsetof(Ctrl, cur_slot)>(ctrl) : ctrl->cur_slot;
   stage_consts_from(fa_words, sc);
   __syncthreads();  // table + constants visible
   const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
@@ -1689,7 +1701,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds sh;
-  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(),
+  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(),
                                                  (int)blockIdx.x, table, prior, w0, w1, part0, part1, bscan0, bscan1,
                                                  gpart0, gpart1, gscan, ctrl, gcount, tcount, prop0, prop1, iter,
                                                  stamps, smem, sc, sh);
@@ -1703,7 +1715,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh(
 // never wait on each other and each one computes exactly what its one-stream frame computes.
 struct Cand;
 template <typename T, typename SP>
-struct StreamDesc {
+struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B words
   FrameArgsT<T> fa;  // first: stage_consts_from reads its head (LdsConst layout)
   const unsigned char* table;
   const SP* prior;
@@ -1734,6 +1746,39 @@ struct StreamDesc {
   int32_t first_blk;  // the stream's first block in the grid
 };
 
+// Batch staging (block s = stream s): the stream's descriptor and, for host-supplied blobs, its table, from
+// the pinned host staging buffer (read over PCIe once) into HBM, and the block -> stream map of its blocks.
+// A launch in the batch's own stream instead of a host-to-device copy: no copy-engine hand-off in front of
+// the weighing launch.  dev / host: the device scratch and its pinned host image (same layout); a table
+// pointer inside [dev, dev + tbytes) is a staged host table.
+template <typename T, typename SP>
+__global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __restrict__ host,
+                                                        unsigned char* __restrict__ dev, uint32_t doff, uint32_t tbytes,
+                                                        uint32_t boff) {
+  typedef __attribute__((address_space(1))) const u32x4_t gv4_t;
+  const int s = blockIdx.x;
+  const StreamDesc<T, SP>* hd = (const StreamDesc<T, SP>*)(host + doff) + s;
+  static_assert(sizeof(StreamDesc<T, SP>) % 16 == 0, "descriptor as 16-B words");
+  {
+    gv4_t* src = (gv4_t*)hd;
+    u32x4_t* dst = (u32x4_t*)((StreamDesc<T, SP>*)(dev + doff) + s);
+    for (int i = threadIdx.x; i < (int)(sizeof(StreamDesc<T, SP>) / 16); i += kBlock) dst[i] = src[i];
+  }
+  const int first = __builtin_amdgcn_readfirstlane(hd->first_blk);
+  const int nblk = __builtin_amdgcn_readfirstlane(hd->fa.nblk);
+  const int B = __builtin_amdgcn_readfirstlane(hd->fa.B);
+  const unsigned char* tab = hd->table;
+  uint16_t* bm = (uint16_t*)(dev + boff);
+  for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
+  const uintptr_t to = (uintptr_t)tab - (uintptr_t)dev;  // wraps above tbytes for bank tables
+  if (to < tbytes) {
+    gv4_t* src = (gv4_t*)(host + to);
+    u32x4_t* dst = (u32x4_t*)(dev + to);
+    const int n4 = (int)(BlobTable<T>::bytes(B) / 16);
+    for (int i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
+  }
+}
+
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) void k_propagate_weigh_multi(const StreamDesc<T, SP>* __restrict__ descs,
                                                                   const uint16_t* __restrict__ bmap, int iter) {
@@ -1741,7 +1786,7 @@ __global__ __launch_bounds__(kBlock) void k_propagate_weigh_multi(const StreamDe
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds sh;
   const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
-  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.table,
+  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP, true>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.table,
                                                  d.prior, d.w0, d.w1, d.part0, d.part1, d.bscan0, d.bscan1, d.gpart0,
                                                  d.gpart1, d.gscan, d.ctrl, d.gcount_w, d.tcount_w, d.prop0, d.prop1,
                                                  iter, nullptr, smem, sc, sh);
@@ -2125,7 +2170,7 @@ __device__ __forceinline__ void resample_phase(
     // regenerated here
     const int loc = cbi - blk * kBlock;
     T Pc[12];
-    if (cbv > 0) {
+    if (cbv > 0 && (!RAW || std::is_same<T, SP>::value)) {  // RAW rows are poses unless the state is fp16 deltas
 #pragma unroll
       for (int q = 0; q < 12; ++q) Pc[q] = sh.rows[loc >> 6][loc & 63].q[q];
     } else {
@@ -2197,7 +2242,7 @@ __device__ __forceinline__ void resample_phase(
 
 // ---- launch 2 of the two-launch path: stratified resampling + winner + frame record.  One block's work
 // (block `blk` of its stream), shared by k_resample and k_resample_multi.
-template <typename T, int RNG, int MAXM, typename SP>
+template <typename T, int RNG, int MAXM, typename SP, bool MULTI>
 __device__ __forceinline__ void resample_block(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post,
@@ -2222,7 +2267,7 @@ __device__ __forceinline__ void resample_block(
   const GroupScan gs = gscan[g];
   T A[12];
   if (!prop0 && valid && n >= 2) load_prior(fa, prior, n, A);
-  const Ctrl c = load_ctrl_uniform(ctrl);
+  const Ctrl c = MULTI ? load_ctrl_uniform(ctrl) : *ctrl;
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
@@ -2260,7 +2305,7 @@ __global__ __launch_bounds__(kBlock) void k_resample(
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
-  resample_block<T, RNG, MAXM, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
+  resample_block<T, RNG, MAXM, SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
                                    table, prior, post, w0, w1, bscan0, bscan1, gscan, cpart, cgroup, gcount, tcount,
                                    counts, cand, mlpose, out, seq, stamps, prop0, prop1, sc, rec, sh);
 }
@@ -2272,7 +2317,7 @@ __global__ __launch_bounds__(kBlock) void k_resample_multi(const StreamDesc<T, S
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
   const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
-  resample_block<T, RNG, MAXM, SP>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.ctrl, d.table,
+  resample_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.ctrl, d.table,
                                    d.prior, d.post, d.w0, d.w1, d.bscan0, d.bscan1, d.gscan, d.cpart, d.cgroup,
                                    d.gcount_r, d.tcount_r, d.counts, d.cand, d.mlpose, d.out, d.seq, nullptr, d.prop0,
                                    d.prop1, sc, rec, sh);
@@ -2282,7 +2327,7 @@ __global__ __launch_bounds__(kBlock) void k_resample_multi(const StreamDesc<T, S
 // index, PE:685-686), its kept-iteration pose regenerated and paired once, then the frame record.  Also
 // reports an unfinished frame (speculative launch) and the re-init branch (PE:707-719).
 constexpr int kFinalBlock = 1024;
-template <typename T, int RNG, int MAXM, typename SP>
+template <typename T, int RNG, int MAXM, typename SP, bool MULTI>
 __device__ __forceinline__ void resample_final_block(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
@@ -2299,7 +2344,7 @@ __device__ __forceinline__ void resample_final_block(
   if (stamps && threadIdx.x == 0) stamps[6] = rt_now();
   // nothing below depends on the control record until the reduction is done: the partial, table and
   // most-likely-pose loads go out together with it (on an unfinished frame they are simply unused)
-  const Ctrl c = load_ctrl_uniform(ctrl);
+  const Ctrl c = MULTI ? load_ctrl_uniform(ctrl) : *ctrl;
   double ml = 0.0;
   if (wv == 0 && lane < 12) ml = mlpose[lane];
   stage_consts_from(fa_words, sc);
@@ -2402,7 +2447,7 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
     const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
     int regen) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  resample_final_block<T, RNG, MAXM, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), ctrl, table, prior,
+  resample_final_block<T, RNG, MAXM, SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), ctrl, table, prior,
                                          cpart, cand, mlpose, out, seq, stamps, regen, smem);
 }
 // batched: block s finishes stream s
@@ -2410,7 +2455,7 @@ template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kFinalBlock) void k_resample_final_multi(const StreamDesc<T, SP>* __restrict__ descs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const StreamDesc<T, SP>& d = descs[blockIdx.x];
-  resample_final_block<T, RNG, MAXM, SP>(d.fa, (const uint32_t*)&d.fa, d.ctrl, d.table, d.prior, d.cpart, d.cand,
+  resample_final_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, d.ctrl, d.table, d.prior, d.cpart, d.cand,
                                          d.mlpose, d.out, d.seq, nullptr, d.prop0 ? 1 : 0, smem);
 }
 

@@ -96,9 +96,11 @@ struct pfmpe_ctx {
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
   // batch scratch (pfmpe_step_multi, owned by the batch's first context): stream descriptors, the
-  // block -> stream map and host-supplied blob tables, staged in pinned memory and copied in one transfer
+  // block -> stream map and host-supplied blob tables; the host writes the descriptors and tables into the
+  // pinned image, a staging launch (k_stage_multi) moves them to HBM and builds the map
   unsigned char* d_multi = nullptr;
   unsigned char* h_multi = nullptr;
+  unsigned char* hd_multi = nullptr;  // device address of h_multi
   size_t multi_cap = 0;
 
   // model / params
@@ -429,7 +431,7 @@ struct Seq {
   // exactly as step()'s two-launch path does for one stream.  h / d: the batch scratch, whose first
   // `tbytes` bytes already hold the host-supplied blob tables; tables[s] are device addresses.
   static int step_multi(pfmpe_ctx* const* cs, int S, const FrameArgsT<T>* fas, const unsigned char* const* tables,
-                        unsigned char* h, unsigned char* d, size_t tbytes) {
+                        unsigned char* h, const unsigned char* hdev, unsigned char* d, size_t tbytes) {
     using Desc = StreamDesc<T, SP>;
     pfmpe_ctx* c0 = cs[0];
     hipStream_t st = c0->stream;
@@ -442,7 +444,6 @@ struct Seq {
       const int na = (int)act.size();
       Desc* hd = (Desc*)(h + doff);
       const size_t boff = doff + (((size_t)na * sizeof(Desc) + 255) / 256) * 256;
-      uint16_t* hb = (uint16_t*)(h + boff);
       int64_t total = 0;
       size_t lds_w = 0, lds_f = 0;
       for (int i = 0; i < na; ++i) {
@@ -479,14 +480,15 @@ struct Seq {
         c->seq = (c->seq + 1) & 0x3fffffff;
         x.seq = c->seq;
         x.first_blk = (int32_t)total;
-        for (int b = 0; b < fa.nblk; ++b) hb[total + b] = (uint16_t)i;
-        total += fa.nblk;
+          total += fa.nblk;
         lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.B));
         lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
       }
-      const size_t end = boff + (size_t)total * sizeof(uint16_t);
-      const size_t from = round == 0 ? 0 : doff;  // the tables travel with the first round's descriptors
-      HIPCHK(c0, hipMemcpyAsync(d + from, h + from, end - from, hipMemcpyHostToDevice, st));
+      // descriptors, host tables (first round) and the block map go to HBM by a staging launch in the same
+      // stream (k_stage_multi reads the pinned image once), not by a copy-engine transfer
+      hipLaunchKernelGGL((k_stage_multi<T, SP>), dim3((unsigned)na), dim3(kBlock), 0, st, hdev, d,
+                         (uint32_t)doff, (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)boff);
+      HIPCHK(c0, hipGetLastError());
       const Desc* dd = (const Desc*)(d + doff);
       const uint16_t* db = (const uint16_t*)(d + boff);
       for (int k = 0; k < nb; ++k, ++iter) {
@@ -584,10 +586,13 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     if (c0->h_multi) HIPCHK(c0, hipHostFree(c0->h_multi));
     c0->d_multi = nullptr;
     c0->h_multi = nullptr;
+    c0->hd_multi = nullptr;
     c0->multi_cap = 0;
     const size_t cap = std::max(need * 2, (size_t)1 << 16);
     HIPCHK(c0, hipMalloc((void**)&c0->d_multi, cap));
-    HIPCHK(c0, hipHostMalloc((void**)&c0->h_multi, cap, hipHostMallocDefault));
+    // read by k_stage_multi over PCIe: mapped, coherent (the host rewrites it between batches)
+    HIPCHK(c0, hipHostMalloc((void**)&c0->h_multi, cap, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(c0, hipHostGetDevicePointer((void**)&c0->hd_multi, c0->h_multi, 0));
     c0->multi_cap = cap;
   }
   std::vector<const unsigned char*> tables(S);
@@ -600,11 +605,11 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
       tables[s] = c0->d_multi + toff[s];
     }
   }
-  if (maxM <= 5) return Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
-  if (maxM <= 8) return Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
+  if (maxM <= 5) return Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  if (maxM <= 8) return Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
   if (maxM <= 12)
-    return Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
-  return Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->d_multi, tbytes);
+    return Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  return Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
 }
 
 template <typename T, int RNG, typename SP>
