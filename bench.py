@@ -153,6 +153,38 @@ def oracle_frames(cfg, n_frames: int, warm: int = 0):
     return statistics.median(times), statistics.median(iters)
 
 
+def _c1_stream_rate(seed: int, n_frames: int):
+    """One process's C1 stream (seeded): (frames, updates, seconds) of the oracle PF block only."""
+    from oracle import pforacle as orc
+    from pf_monocular_pose_estimator_amd import synthetic as syn
+    c1 = syn.CONFIGS["C1"]
+    cfg = syn.StreamConfig(c1.name, M=c1.M, B=c1.B, N=c1.N, seed=seed)
+    st = syn.make_stream(cfg, n_frames + 5)
+    prior = st.prior()
+    tot, upd = 0.0, 0
+    for fr in st.frames:
+        t0 = time.perf_counter()
+        out, arr = orc.pf_step(st.markers, st.K, orc.make_params(), prior, fr.current_pose, fr.predicted_pose,
+                               fr.prediction, fr.blobs, dt=fr.dt, seed=11 + fr.index, frame_idx=fr.index)
+        if fr.index >= 5:
+            tot += time.perf_counter() - t0
+            upd += cfg.N * out["iters"]
+        if out["resampled"]:
+            prior = arr["resampled"]
+    return n_frames, upd, tot
+
+
+def cpu_multiprocess(procs: int, n_frames: int):
+    """SURVEY.md §8(d)'s multi-core CPU comparison: one process per core on independent C1 streams, aggregate
+    updates/s = sum over processes of (updates / own PF-block time)."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.starmap(_c1_stream_rate, [(100 + i, n_frames) for i in range(procs)])
+    return {"procs": procs, "value": sum(u / t for _, u, t in res), "unit": "particle-updates/s",
+            "sample": f"C1 x {procs} independent streams, {n_frames} frames each after 5 warm-up, one process each"}
+
+
 def cpu_baseline(cfg, n_frames: int, c1_frames: int):
     from pf_monocular_pose_estimator_amd import synthetic as syn
     model, ncpu = host_cpu()
@@ -170,6 +202,7 @@ def cpu_baseline(cfg, n_frames: int, c1_frames: int):
                      "ms_per_frame": t1 * 1e3, "iters_per_frame": k1,
                      "sample": f"C1 (N={c1.N}, M={c1.M}, B={c1.B}): median of {c1_frames} frames after 20 warm-up, "
                                f"1 thread"}
+        res["c1_multiprocess"] = cpu_multiprocess(min(8, ncpu or 1), 50)
     return res
 
 
@@ -194,7 +227,7 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
                        sid0: int, prune: int, keep_prop: int):
     """S independent streams of `base` on one GPU, each frame of all S run as ONE batch (pfmpe_step_multi:
     one weighing launch over every stream's blocks, one resampling launch, one finishing launch).  Blob tables
-    come from each stream's staged bank; the loop calls the C-ABI directly (one FFI call per batch)."""
+    come from each stream's staged bank; the timed loop is pfmpe_step_multi_batch (the C loop a tracker runs)."""
     import ctypes as C
     engs, frames = [], []
     n = warmup + steps
@@ -217,16 +250,18 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
                                           frame_idx=f.index) for f in st.frames])
         lib = engs[0].lib
         ctxs = (C.c_void_p * S)(*[e.ctx.value for e in engs])
-        ins = [(pf.FrameIn * S)(*[frames[s][f] for s in range(S)]) for f in range(n)]
-        outs = [(pf.FrameOut * S)() for _ in range(n)]
-        for f in range(warmup):
-            engs[0]._chk(lib.pfmpe_step_multi(ctxs, S, ins[f], outs[f]))
-        t0 = time.perf_counter()
-        for f in range(warmup, n):
-            engs[0]._chk(lib.pfmpe_step_multi(ctxs, S, ins[f], outs[f]))
+        ins = (pf.FrameIn * (S * n))(*[frames[s][f] for f in range(n) for s in range(S)])  # batch-major
+        outs = (pf.FrameOut * (S * n))()
+        done = C.c_int()
+        fin, fout = C.sizeof(pf.FrameIn), C.sizeof(pf.FrameOut)
+        at_in = lambda f: C.cast(C.byref(ins, f * S * fin), C.POINTER(pf.FrameIn))  # noqa: E731
+        at_out = lambda f: C.cast(C.byref(outs, f * S * fout), C.POINTER(pf.FrameOut))  # noqa: E731
+        engs[0]._chk(lib.pfmpe_step_multi_batch(ctxs, S, at_in(0), warmup, at_out(0), C.byref(done)))
+        t0 = time.perf_counter()  # the C loop a multi-object tracker runs: every batch blocks on its records
+        engs[0]._chk(lib.pfmpe_step_multi_batch(ctxs, S, at_in(warmup), steps, at_out(warmup), C.byref(done)))
         el = time.perf_counter() - t0
-        upd = sum(base.N * o.iters for f in range(warmup, n) for o in outs[f])
-        acc = sum(o.accepted for f in range(warmup, n) for o in outs[f])
+        upd = sum(base.N * outs[i].iters for i in range(warmup * S, n * S))
+        acc = sum(outs[i].accepted for i in range(warmup * S, n * S))
         return {"streams": S, "N_per_stream": base.N, "live_particles": S * base.N,
                 "updates_per_s": upd / el, "ms_per_batch": el * 1e3 / steps,
                 "frames_per_sec_per_stream": steps / el, "accept_rate": acc / (S * steps)}

@@ -150,6 +150,12 @@ int pfmpe_step_batch(pfmpe_ctx* ctx, const pfmpe_frame_in* in, int n, pfmpe_fram
  * mismatch (nothing launched), or the failing stream's error text in pfmpe_last_error(ctxs[0]). */
 int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pfmpe_frame_out* out);
 
+/* n consecutive batches of pfmpe_step_multi (in / out: n x S, batch-major), each blocking on its records
+ * before the next is launched — the loop a multi-object C/C++ tracker runs, without per-call FFI overhead.
+ * Stops at the first error; *done receives the number of batches completed. */
+int pfmpe_step_multi_batch(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out,
+                           int* done);
+
 /* ---------------------------------------------------------------------- ROI prediction (§8f row 1) */
 /* predictMarkerPositionsInImage (PE:1036-1053) + LEDDetector::determineROI (led_detector.cpp:217-369),
  * as called at PE:396-412: every marker projected through camMoveInv * prior_j * predictionMatrix for all

@@ -32,7 +32,7 @@ K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK
 EXPORTED_SYMBOLS = (
     "pfmpe_create", "pfmpe_destroy", "pfmpe_last_error", "pfmpe_abi_version",
     "pfmpe_set_model", "pfmpe_set_params", "pfmpe_default_params", "pfmpe_set_prior",
-    "pfmpe_step", "pfmpe_step_batch", "pfmpe_step_multi", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
+    "pfmpe_step", "pfmpe_step_batch", "pfmpe_step_multi", "pfmpe_step_multi_batch", "pfmpe_get_particles", "pfmpe_get_weights", "pfmpe_get_counts",
     "pfmpe_set_option", "pfmpe_stage_blob_bank", "pfmpe_get_kernel_stats",
     "pfmpe_reset_kernel_stats", "pfmpe_kernel_name", "pfmpe_host_ref_uniform", "pfmpe_host_philox",
     "pfmpe_predict_roi", "pfmpe_default_init_params", "pfmpe_p3p_histogram", "pfmpe_initialise",
@@ -162,6 +162,7 @@ def load() -> C.CDLL:
         "pfmpe_step": (I, [P, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
         "pfmpe_step_batch": (I, [P, C.POINTER(FrameIn), I, C.POINTER(FrameOut), C.POINTER(I)]),
         "pfmpe_step_multi": (I, [C.POINTER(P), I, C.POINTER(FrameIn), C.POINTER(FrameOut)]),
+        "pfmpe_step_multi_batch": (I, [C.POINTER(P), I, C.POINTER(FrameIn), I, C.POINTER(FrameOut), C.POINTER(I)]),
         "pfmpe_get_particles": (I, [P, I, dp]),
         "pfmpe_get_weights": (I, [P, dp]),
         "pfmpe_get_counts": (I, [P, C.POINTER(C.c_uint32)]),

@@ -446,6 +446,18 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
   return PFMPE_OK;
 }
 
+int pfmpe_step_multi_batch(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out,
+                           int* done) {
+  if (done) *done = 0;
+  if (!ctxs || S < 1 || !ctxs[0]) return PFMPE_E_ARG;
+  if ((!in || !out) && n > 0) return fail(ctxs[0], PFMPE_E_ARG, "step_multi_batch: null in/out");
+  for (int f = 0; f < n; ++f) {
+    RET(pfmpe_step_multi(ctxs, S, in + (size_t)f * S, out + (size_t)f * S));
+    if (done) *done = f + 1;
+  }
+  return PFMPE_OK;
+}
+
 int pfmpe_step_batch(pfmpe_ctx* c, const pfmpe_frame_in* in, int n, pfmpe_frame_out* out, int* done) {
   if (!c) return PFMPE_E_ARG;
   if (done) *done = 0;
