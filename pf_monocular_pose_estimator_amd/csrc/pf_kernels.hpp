@@ -2356,16 +2356,25 @@ __device__ __forceinline__ void resample_final_block(
   }
   int bv = -1, bi = 0x7fffffff;
   {
+    // two partials per 16-B load, eight predicated loads in flight per thread (C4: 39k partials in about
+    // three round trips); the buffer holds one spare partial for an odd count (pfmpe_create)
     const int nb = fa.nblk;
-    for (int base = (int)threadIdx.x; base < nb; base += 4 * kFinalBlock) {  // four predicated loads in flight
-      CountPart p[4];
+    const int n2 = (nb + 1) / 2;
+    const u32x4_t* cp4 = (const u32x4_t*)cpart;
+    for (int base = (int)threadIdx.x; base < n2; base += 8 * kFinalBlock) {
+      u32x4_t p[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int i = base + u * kFinalBlock;
-        p[u] = i < nb ? cpart[i] : CountPart{-1, 0x7fffffff};
+        const u32x4_t none = {0xffffffffu, 0x7fffffffu, 0xffffffffu, 0x7fffffffu};
+        p[u] = i < n2 ? cp4[i] : none;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) cmb_max(bv, bi, p[u].maxcount, p[u].idx);
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * kFinalBlock;
+        cmb_max(bv, bi, (int)p[u].x, (int)p[u].y);
+        if (2 * i + 1 < nb) cmb_max(bv, bi, (int)p[u].z, (int)p[u].w);
+      }
     }
     wave_argmax(bv, bi);
     if (lane == 0) {

@@ -213,7 +213,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
     ok &= hipMalloc((void**)&c->d_gpart[i], (size_t)c->max_grp * sizeof(GroupPart)) == hipSuccess;
   }
   ok &= hipMalloc((void**)&c->d_gscan, (size_t)c->max_grp * sizeof(GroupScan)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_cpart, (size_t)c->max_blk * sizeof(CountPart)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_cpart, (size_t)(c->max_blk + 1) * sizeof(CountPart)) == hipSuccess;  // +1: 16-B reads
   ok &= hipMalloc((void**)&c->d_cgroup, (size_t)c->max_grp * sizeof(CountPart)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_counters, counters_bytes(c)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
