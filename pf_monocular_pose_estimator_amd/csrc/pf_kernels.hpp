@@ -66,6 +66,7 @@ struct FrameArgsT {
   T markers[kMaxMarkers * 3];
   T K[9];
   T lo[6], hi[6];           // draw ranges angX angY angZ tX tY tZ (scaled by fac*), Philox stream
+  T rg[6];                  // hi - lo, rounded once on the host (the fp32 Philox draw is lo + u * rg)
   double dlo[6], dhi[6];    // the same in double, reference stream (draws are computed in double)
   double growth;            // 0.025
   T tol, tol_pf, tolq;      // score normaliser / acceptance gate / pruning half-window
@@ -77,6 +78,7 @@ struct FrameArgsT {
   int32_t cam_identity, max_iter, force_iters, nblk;
   int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
   int32_t diag;                   // diagnostic switches (0 in production; pfmpe_ctx.hpp kDiag*)
+  int32_t small_angles;           // every angle draw of the frame has |x| <= kSmallAngle (host bound, fp32)
   uint32_t wait_ticks;            // bound of every in-launch wait, s_memrealtime ticks (100 MHz)
   uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
   int64_t ld;                     // SoA plane stride in elements
@@ -91,6 +93,7 @@ struct LdsConst {
   T markers[kMaxMarkers * 3];
   T K[9];
   T lo[6], hi[6];
+  T rg[6];
 };
 
 // Per-frame control record.  All-zero is the valid "start of frame" state (zeroed at create, set_prior
@@ -169,10 +172,19 @@ __device__ __forceinline__ void sincos_t(float x, float* s, float* c) {
     sincosf(x, s, c);
   }
 }
+// |x| <= kSmallAngle (the host proves it for every angle draw of a frame: FrameArgsT::small_angles): the
+// next Taylor terms are below half an fp32 ulp there (x^5/120 / x <= 6.8e-9, x^6/720 <= 1e-12)
+constexpr float kSmallAngle = 0.03f;
+__device__ __forceinline__ void sincos_small(float x, float* s, float* c) {
+  const float x2 = x * x;
+  *s = x * fmadd(x2, -1.0f / 6.0f, 1.0f);
+  *c = fmadd(x2, fmadd(x2, 1.0f / 24.0f, -0.5f), 1.0f);
+}
 __device__ __forceinline__ void sincos_t(double x, double* s, double* c) {
   *s = sin(x);
   *c = cos(x);
 }
+__device__ __forceinline__ void sincos_small(double x, double* s, double* c) { sincos_t(x, s, c); }  // fp64: exact path
 // fp32: the hardware square root (v_sqrt_f32, 1 ulp) instead of sqrtf's correctly rounded 14-instruction
 // sequence (tolerance path, like div_t); fp64 stays IEEE
 // max / min for the wave extrema (operands are never NaN: weights are finite, identities are +-inf)
@@ -208,7 +220,8 @@ __device__ __forceinline__ T inf_t() {
 // lane (no SGPR round trip: kept in SGPRs they spill into VGPR lanes).  Callers barrier afterwards.
 template <typename T>
 __device__ __forceinline__ void stage_consts_from(const uint32_t* src, LdsConst<T>& sc) {
-  static_assert(offsetof(FrameArgsT<T>, cur) == 0 && offsetof(FrameArgsT<T>, hi) == offsetof(LdsConst<T>, hi),
+  static_assert(offsetof(FrameArgsT<T>, cur) == 0 && offsetof(FrameArgsT<T>, hi) == offsetof(LdsConst<T>, hi) &&
+                    offsetof(FrameArgsT<T>, rg) == offsetof(LdsConst<T>, rg),
                 "LdsConst must mirror the head of FrameArgsT");
   static_assert(sizeof(LdsConst<T>) % 4 == 0, "dword copy");
   uint32_t* dst = (uint32_t*)&sc;
@@ -388,14 +401,20 @@ __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsCons
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
       const T u = u21_t<T>(r.v[q]);  // exact in either type
-      const T draw = u * (sc.hi[q] - sc.lo[q]) + sc.lo[q];
+      const T draw = u * sc.rg[q] + sc.lo[q];  // rg = hi - lo (host), the same value the device formed
       d[q] = draw * g;
     }
   }
   T sa, ca, sb, cb, sz, cz;
-  sincos_t(d[0], &sa, &ca);
-  sincos_t(d[1], &sb, &cb);
-  sincos_t(d[2], &sz, &cz);
+  if (fa.small_angles) {  // wave-uniform (fp32 only: the host never sets it for fp64)
+    sincos_small(d[0], &sa, &ca);
+    sincos_small(d[1], &sb, &cb);
+    sincos_small(d[2], &sz, &cz);
+  } else {
+    sincos_t(d[0], &sa, &ca);
+    sincos_t(d[1], &sb, &cb);
+    sincos_t(d[2], &sz, &cz);
+  }
   // R = ((R_A * Rz(c)) * Ry(b)) * Rx(a)   (PE:582)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -718,9 +737,13 @@ __device__ __forceinline__ float score_unordered(const FrameArgsT<float>& fa, co
 #pragma unroll
     for (int e = 0; e < j; ++e) dup |= acc[e] & (r[e] == r[j]);
     dups += (acc[j] & dup) ? 1 : 0;
-    if ((fa.downgrade >> j) & 1u) Pr = acc[j] ? Pr - 2.0f : Pr;
   }
-  return Pr - (float)(3 * dups * (dups + 1) / 2);
+  int ndg = 0;
+  if (fa.downgrade) {  // wave-uniform: the downgrade penalties (2 per accepted downgraded marker)
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) ndg += (acc[j] && ((fa.downgrade >> j) & 1u)) ? 1 : 0;
+  }
+  return Pr - (float)(3 * dups * (dups + 1) / 2 + 2 * ndg);
 }
 
 // ----------------------------------------------------------------------------- wave/block helpers
@@ -1526,42 +1549,49 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
 //  * max / min of the weights: value-only DPP reductions (max and min do not round, so any order is exact),
 //    interleaved with the sum scan; argmax / argmin = the first valid lane holding that value (ballot),
 //    i.e. the lowest particle index, exactly the lexicographic (value, index) order of cmb_max / cmb_min.
+//  * min / argmin are only needed on the re-initialisation branch when the weight sum is negative (PE:714:
+//    the most likely particle is the argmax of the normalised weights), and then the global minimum is
+//    negative and lies in a wave holding a negative weight.  So a wave without negative weights reports
+//    (+inf, none) and skips the min reduction (wave-uniform branch): the global argmin is unchanged.
 //  * extrema of wi: when no valid weight is negative the DPP prefix is non-decreasing over the lanes (each
 //    row_shr / row_bcast step adds a non-negative, lane-monotone addend, and rounding is monotone), so the
 //    maximum is lane 63's total and the minimum lane 0's value (valid lanes are a prefix of the wave).
-//    Only a wave holding a negative weight runs the two prefix max/min scans (wave-uniform branch).
+//    Only a wave holding a negative weight runs the two prefix max/min scans.
 template <typename T>
 __device__ __forceinline__ void wave_weight_partials(T w, bool valid, int n, double& wi, double& rmx, double& rmn,
                                                      T& mx, int& ix, T& mn, int& in_) {
   wi = valid ? (double)w : 0.0;
   mx = valid ? w : -inf_t<T>();
-  mn = valid ? w : inf_t<T>();
+  const bool neg = __ballot(valid && w < (T)0) != 0;  // wave-uniform
   scan_steps([&](auto st) {
     using S = decltype(st);
     st_sum<S>(wi);
     mx = fmax_t(mx, dpp<S::ctrl, S::rm>(mx, -inf_t<T>()));
-    mn = fmin_t(mn, dpp<S::ctrl, S::rm>(mn, inf_t<T>()));
   });
   mx = lane_value(mx, 63);
-  mn = lane_value(mn, 63);
   const uint64_t bx = __ballot(valid && w == mx);
-  const uint64_t bn = __ballot(valid && w == mn);
   ix = bx ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bx)) : 0x7fffffff;
-  in_ = bn ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bn)) : 0x7fffffff;
+  mn = inf_t<T>();
+  in_ = 0x7fffffff;
   if (!bx) {  // no valid lane
     rmx = -INFINITY;
     rmn = INFINITY;
-  } else if (mn >= (T)0) {
+  } else if (!neg) {
     rmx = lane_value(wi, 63);
     rmn = lane_value(wi, 0);
   } else {
+    mn = valid ? w : inf_t<T>();
     rmx = valid ? wi : -INFINITY;
     rmn = valid ? wi : INFINITY;
     scan_steps([&](auto st) {
       using S = decltype(st);
+      mn = fmin_t(mn, dpp<S::ctrl, S::rm>(mn, inf_t<T>()));
       st_max<S>(rmx);
       st_min<S>(rmn);
     });
+    mn = lane_value(mn, 63);
+    const uint64_t bn = __ballot(valid && w == mn);
+    in_ = bn ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bn)) : 0x7fffffff;
     rmx = lane_value(rmx, 63);
     rmn = lane_value(rmn, 63);
   }

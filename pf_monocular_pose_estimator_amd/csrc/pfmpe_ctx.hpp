@@ -654,8 +654,16 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   for (int q = 0; q < 6; ++q) {
     fa.lo[q] = (T)fa.dlo[q];
     fa.hi[q] = (T)fa.dhi[q];
+    fa.rg[q] = (T)(fa.hi[q] - fa.lo[q]);  // in T: the value the device formed before (bit-identical draws)
   }
   fa.growth = p.growth;
+  {  // fp32: every angle draw of the frame within kSmallAngle -> the short sincos polynomials (wave-uniform)
+    const int cap = in->force_iters > 0 ? in->force_iters : std::max(1, p.max_iter);
+    const double gmax = 1.0 + p.growth * (double)((cap - 1) / 10);
+    double amax = 0.0;
+    for (int q = 0; q < 3; ++q) amax = std::max(amax, std::max(std::abs(fa.dlo[q]), std::abs(fa.dhi[q])));
+    fa.small_angles = (sizeof(T) == 4 && amax * std::abs(gmax) <= 0.999 * (double)kSmallAngle) ? 1 : 0;
+  }
   fa.tol = (T)p.tol;
   fa.tol_pf = (T)p.tol_pf;
   // every blob with sqrt(d2) <= tol_pf (in T arithmetic) has |dx| <= tolq
