@@ -23,7 +23,7 @@ FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED = 1, 2, 3, 4, 5
 OPT_WAIT_BOUND_US, OPT_FUSED_REARM = 6, 7
 OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
-DIAG_LAG_LOADS, DIAG_ABANDON = 64, 128
+DIAG_LAG_LOADS, DIAG_ABANDON, DIAG_NO_STREAM, DIAG_FORCE_STREAM = 64, 128, 512, 1024
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
 INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N = 1, 2, 3, 4, 5
 K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)

@@ -1097,7 +1097,9 @@ enum : int {
   kDiagSqrtGroups = 32, // groups of ~sqrt(nblk) blocks even when the frame fits k_frame2
   kDiagLagLoads = 64,   // k_frame2: the last block sleeps ~20 us before loading the block partials
   kDiagAbandon = 128,   // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
-  kDiagSortedScore = 256  // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
+  kDiagSortedScore = 256, // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
+  kDiagNoStream = 512,     // two-launch path: never the streaming weighing pass (k_weigh_stream + k_group + k_top)
+  kDiagForceStream = 1024  // two-launch path: always the streaming weighing pass (tests / A/B)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -1395,7 +1397,8 @@ template <typename T, int RNG>
 __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __restrict__ ctrl, int iter,
                                               const GroupPart* __restrict__ gp0, const GroupPart* __restrict__ gp1,
                                               GroupScan* __restrict__ gscan, uint32_t* __restrict__ gen,
-                                              uint32_t gen_base, const GroupPart cur, bool have_cur, int slot) {
+                                              uint32_t gen_base, const GroupPart cur, bool have_cur, int slot,
+                                              const GroupPart* lds_cur = nullptr) {
   const int lane = lane_id();
   const int ngrp = fa.ngrp;
   // <= 64 groups: each lane's group partial of this iteration is loaded ONCE, in the same round trip as
@@ -1419,7 +1422,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
   } else {
     const GroupPart* P = slot ? gp1 : gp0;
     for (int g = lane; g < ngrp; g += 64) {
-      const GroupPart q = group_part(P, g, cur, have_cur);
+      const GroupPart q = lds_cur ? lds_cur[g] : group_part(P, g, cur, have_cur);
       cmb_max(mv, mi, q.maxw, q.argmax);
     }
   }
@@ -1445,7 +1448,10 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
     // kept slot's partials of a one-tile frame: this iteration's (registers) or an earlier one's (load)
     GroupPart kq = q0;
     if (one_tile && c.kept_slot != slot && lane < ngrp) kq = group_part(KG, lane, cur, kreg);
-    auto kept_part = [&](int g) -> GroupPart { return one_tile ? kq : group_part(KG, g, cur, kreg); };
+    const bool kept_lds = lds_cur && c.kept_slot == slot;  // this iteration's parts, staged in LDS
+    auto kept_part = [&](int g) -> GroupPart {
+      return one_tile ? kq : (kept_lds ? lds_cur[g] : group_part(KG, g, cur, kreg));
+    };
 
     // S = total over groups (tiles of 64 groups, carried)
     double carry = 0.0;
@@ -1669,6 +1675,150 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
   if (stamps && lane == 0) stamps[2] = rt_now();
   propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, gen, gen_base, gr, single, slot);
   if (stamps && lane == 0) stamps[3] = rt_now();
+}
+
+// ---- the streaming weighing pass (two-launch path, one stream): a grid of at most a few blocks per CU,
+// each looping over the frame's 256-particle blocks vb = blockIdx.x, + gridDim.x, ...  The next block's
+// prior loads are issued before this block's weights are stored and scanned, so the HBM latency of the
+// state hides behind the arithmetic; the table and the frame constants are staged once per physical block;
+// the block partials are plain stores read by k_group_top after the launch boundary (no arrival counters,
+// no group / top tail in this launch).  Per 256-particle block the arithmetic and the partial are exactly
+// k_propagate_weigh's, so the weights, partials and every later decision are bit-identical.
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) void k_weigh_stream(const FrameArgsT<T> fa, const unsigned char* __restrict__ table,
+                                                         const SP* __restrict__ prior, T* __restrict__ w0,
+                                                         T* __restrict__ w1, BlockPart* __restrict__ part0,
+                                                         BlockPart* __restrict__ part1, const Ctrl* __restrict__ ctrl,
+                                                         SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<T> sc;
+  __shared__ WeighLds sh;
+  if (ctrl->done) return;  // the exit rule already fired (uniform)
+  const int slot = ctrl->cur_slot;
+  T* wout = slot ? w1 : w0;
+  SP* pout = slot ? prop1 : prop0;
+  BlockPart* parts = slot ? part1 : part0;
+  const int lane = lane_id(), wv = wave_id();
+  int vb = (int)blockIdx.x;
+  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  // raw state values of this block's particle (converted where they are used), so the loads of the next
+  // block's particle can stay in flight across a whole block's arithmetic
+  SP R[12];
+  {
+    const int n = vb * kBlock + (int)threadIdx.x;
+    if (n < fa.N && n >= 2) load_state_raw<SP>(prior, fa.ld, n, R);
+  }
+  stage_consts(fa, sc);
+  __syncthreads();  // table + constants visible
+  const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
+  const int step = (int)gridDim.x * kBlock;
+  for (; vb < fa.nblk; vb += (int)gridDim.x) {
+    const int n = vb * kBlock + (int)threadIdx.x;
+    const bool valid = n < fa.N;
+    T A[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(R[q], fa.anc_in[q]);
+    if (n + step < fa.N && n + step >= 2) load_state_raw<SP>(prior, fa.ld, n + step, R);  // next block's particle
+    T w = (T)0, P[12];
+    if (valid) w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
+    if (valid) {
+      wout[n] = w;
+      if (prop0) store_pose<T, SP>(pout, fa.ld, n, P, fa.anc_out);
+    }
+    double wi, rmx, rmn;
+    T mx, mn;
+    int ix, in_;
+    wave_weight_partials(w, valid, n, wi, rmx, rmn, mx, ix, mn, in_);
+    if (lane == 63) sh.tot[wv] = wi;
+    if (lane == 0) {
+      sh.rmax[wv] = rmx;
+      sh.rmin[wv] = rmn;
+      sh.mx[wv] = (double)mx;
+      sh.mn[wv] = (double)mn;
+      sh.ix[wv] = ix;
+      sh.in_[wv] = in_;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // publish_iteration's block partial, same association
+      double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = sh.mx[0], bmn = sh.mn[0];
+      int bix = sh.ix[0], bin = sh.in_[0];
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        const double a = pre + sh.rmax[ww], b = pre + sh.rmin[ww];
+        maxrel = a > maxrel ? a : maxrel;
+        minrel = b < minrel ? b : minrel;
+        if (ww) {
+          cmb_max(bmx, bix, sh.mx[ww], sh.ix[ww]);
+          cmb_min(bmn, bin, sh.mn[ww], sh.in_[ww]);
+        }
+        pre = pre + sh.tot[ww];
+      }
+      BlockPart q;
+      q.sum = pre;
+      q.maxrel = maxrel;
+      q.minrel = minrel;
+      q.maxw = bmx;
+      q.minw = bmn;
+      q.argmax = bix;
+      q.argmin = bin;
+      parts[vb] = q;
+    }
+    __syncthreads();  // sh is reused by the next block
+  }
+}
+
+// ---- the iteration's group / top hand-off after a streaming weighing pass, as two small launches with no
+// arrival counters (all groups finish at once here, and one counter taking ngrp arrivals back to back
+// serialises them, ~25 ns each): k_group, block g (one wave) scans group g's block partials exactly as
+// publish_iteration's last arriver does (propagate_group); k_top (one wave) runs propagate_top, with every
+// group partial of the iteration staged in LDS in one round trip when there is more than one tile of groups.
+// Same functions, same association as the other frame shapes.
+template <typename T>
+__global__ __launch_bounds__(64) void k_group(const FrameArgsT<T> fa, BlockPart* __restrict__ part0,
+                                              BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0,
+                                              BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+                                              GroupPart* __restrict__ gpart1, const Ctrl* __restrict__ ctrl) {
+  if (ctrl->done) return;
+  const int slot = ctrl->cur_slot;
+  (void)propagate_group(fa.nblk, fa.gsz, (int)blockIdx.x, slot ? part1 : part0, slot ? bscan1 : bscan0,
+                        slot ? gpart1 : gpart0);
+}
+template <typename T, int RNG>
+__global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
+                                            GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                            Ctrl* __restrict__ ctrl, int iter, int lds_groups) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // lds_groups: ngrp entries
+  if (ctrl->done) return;
+  const int slot = ctrl->cur_slot;
+  const GroupPart* src = slot ? gpart1 : gpart0;
+  GroupPart none;
+  none.sum = 0.0;
+  none.zmax = -INFINITY;
+  none.zmin = INFINITY;
+  none.maxw = -INFINITY;
+  none.minw = INFINITY;
+  none.argmax = none.argmin = 0x7fffffff;
+  const bool single = fa.ngrp == 1;
+  const GroupPart g0 = single ? group_part(src, 0, none, false) : none;  // the one group's partial
+  const GroupPart* staged = nullptr;
+  if (fa.ngrp > 64 && lds_groups) {
+    for (int base = 0; base < fa.ngrp; base += 64 * 8) {
+      GroupPart q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int gg = base + u * 64 + lane_id();
+        if (gg < fa.ngrp) q[u] = group_part(src, gg, none, false);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int gg = base + u * 64 + lane_id();
+        if (gg < fa.ngrp) gsm[gg] = q[u];
+      }
+    }
+    wave_lds_sync();
+    staged = gsm;
+  }
+  propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, nullptr, 0u, g0, single, slot, staged);
 }
 
 // ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread.

@@ -268,6 +268,44 @@ struct Seq {
     RET(ensure_prop(c));
     SP* prop0 = c->keep_prop ? (SP*)c->d_prop[0] : nullptr;
     SP* prop1 = c->keep_prop ? (SP*)c->d_prop[1] : nullptr;
+    // The streaming weighing pass (k_weigh_stream: resident blocks looping over the 256-particle blocks, the
+    // next particle's state prefetched) with the group / top hand-off as two small launches.  It wins where
+    // the weighing waits on HBM and the top is one tile of groups: <= 8 markers and <= 64 groups (N <= 1M;
+    // C5: 52 -> 31 us weighing, 104 -> 95 us per frame).  At 12 markers (C3) the weighing is VALU bound and
+    // the extra launches cost more than the prefetch saves; beyond one tile (C4, 611 groups) the separate
+    // group / top launches take back what the weighing saves.
+    const bool stream = !(c->diag & kDiagNoStream) && ((c->diag & kDiagForceStream) || (MAXM <= 8 && fa.ngrp <= 64));
+    if (stream) {
+      const void* fn = c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
+                                : (const void*)k_weigh_stream<T, RNG, MAXM, false, SP>;
+      auto key = std::make_pair(fn, lds);
+      auto it = c->occ.find(key);
+      if (it == c->occ.end()) {
+        int per_cu = 0;
+        HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds));
+        it = c->occ.emplace(key, std::max(1, per_cu)).first;
+      }
+      const int grid = std::min(fa.nblk, it->second * std::max(1, c->num_cu));
+      RET(launch(c, PFMPE_K_PROPAGATE, [&] {
+        if (c->prune)
+          hipLaunchKernelGGL((k_weigh_stream<T, RNG, MAXM, true, SP>), dim3(grid), dim3(kBlock), lds, c->stream, fa,
+                             table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_ctrl, prop0,
+                             prop1, iter);
+        else
+          hipLaunchKernelGGL((k_weigh_stream<T, RNG, MAXM, false, SP>), dim3(grid), dim3(kBlock), lds, c->stream, fa,
+                             table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_ctrl, prop0,
+                             prop1, iter);
+      }));
+      // the top's group partials fit LDS up to 1,365 groups (22M particles); beyond, it reads them from L2
+      const size_t glds = fa.ngrp > 64 ? (size_t)fa.ngrp * sizeof(GroupPart) : 0;
+      const bool staged = glds > 0 && glds <= 64 * 1024;
+      return launch(c, PFMPE_K_AUX, [&] {
+        hipLaunchKernelGGL((k_group<T>), dim3(fa.ngrp), dim3(64), 0, c->stream, fa, c->d_part[0], c->d_part[1],
+                           c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], (const Ctrl*)c->d_ctrl);
+        hipLaunchKernelGGL((k_top<T, RNG>), dim3(1), dim3(64), staged ? glds : 0, c->stream, fa, c->d_gpart[0],
+                           c->d_gpart[1], c->d_gscan, c->d_ctrl, iter, staged ? 1 : 0);
+      });
+    }
     return launch(c, PFMPE_K_PROPAGATE, [&] {
       if (c->prune)
         hipLaunchKernelGGL((k_propagate_weigh<T, RNG, MAXM, true, SP>), dim3(fa.nblk), dim3(kBlock), lds, c->stream, fa,

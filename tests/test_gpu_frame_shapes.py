@@ -220,3 +220,48 @@ def test_c3_full_size_properties():
 
 def test_c4_full_size_properties():
     _full_size_properties("C4", pf.STATE_F16, 0.002)
+
+
+@pytest.mark.parametrize("state,N,M,B,heavy", [(pf.STATE_F64, 140_000, 5, 50, False),
+                                               (pf.STATE_F32, 1_200_000, 5, 50, False),
+                                               (pf.STATE_F16, 1_200_000, 12, 200, True)])
+def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy):
+    """The two-launch path's streaming weighing pass (k_weigh_stream + k_group + k_top: resident blocks
+    looping over the 256-particle blocks, the next particle's state prefetched) against the
+    one-block-per-256-particles k_propagate_weigh: identical records, weights, propagated and resampled sets
+    over a steady frame and an 80-iteration frame (one LED hidden), one tile of groups (140k) and several
+    (1.2M: 4,688 blocks in 74 groups), fp64 / fp32 / fp16 state."""
+    cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
+    st = syn.make_stream(cfg, 2)
+    prior = st.prior(fast=True)
+    res = []
+    for diag in (pf.DIAG_FORCE_STREAM, pf.DIAG_NO_STREAM):
+        eng = make_engine(N, st.markers, st.K, state, pf.RNG_PHILOX, fused=0)
+        eng.set_option(pf.OPT_DIAG, diag)
+        eng.set_prior(prior)
+        snaps = []
+        for f, fr in enumerate(st.frames):
+            blobs = fr.blobs
+            kw = {}
+            if f == 1:  # LED 0's blob hidden: all 80 iterations, the kept slot moves (forced with clutter)
+                uv0 = syn.project(st.K, fr.truth, st.markers)[0]
+                blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
+                kw = {"force_iters": 80} if heavy else {}
+            out = eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=blobs, dt=fr.dt,
+                                          seed=77 + f, frame_idx=f, **kw)).as_dict()
+            snap = {"out": out, "w": eng.get_weights(), "p0": eng.get_particles(0)}
+            if out["resampled"]:
+                snap["p1"] = eng.get_particles(1)
+                snap["counts"] = eng.get_counts()
+            snaps.append(snap)
+        assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+        eng.close()
+        res.append(snaps)
+    assert res[0][1]["out"]["iters"] == 80
+    for a, b in zip(*res):
+        for k, v in a["out"].items():
+            assert np.array_equal(np.asarray(v), np.asarray(b["out"][k])), k
+        for k in ("w", "p0", "p1", "counts"):
+            assert (k in a) == (k in b)
+            if k in a:
+                assert np.array_equal(a[k], b[k]), k
