@@ -342,6 +342,7 @@ def main():
                                                   for o in outs],
                        "post_sha1": hashlib.sha1(post.tobytes()).hexdigest()}, f)
     shape = eng.info(pf.INFO_LAST_SHAPE)
+    weigh_pass = eng.info(pf.INFO_LAST_WEIGH_PASS)
     fallbacks = eng.info(pf.INFO_FUSED_FALLBACKS)
 
     elapsed, total_updates = combine_ranks(dist, elapsed, updates)
@@ -377,6 +378,9 @@ def main():
         ab = algorithmic_bytes(S, cfg.N, k_mean)
         roof = None
         timed = {k: v for k, v in stats.items() if v[0] > 0}
+        if weigh_pass == pf.WEIGH_STREAM and "k_propagate_weigh" in timed:  # the streaming weighing pass
+            timed["k_weigh_stream"] = timed.pop("k_propagate_weigh")
+            ab["k_weigh_stream"] = ab["k_propagate_weigh"]
         if timed:
             dom = max(timed, key=lambda k: timed[k][1])
             launches, ms = timed[dom]

@@ -25,7 +25,8 @@ OPT_WAIT_BOUND_US, OPT_FUSED_REARM = 6, 7
 OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
 DIAG_LAG_LOADS, DIAG_ABANDON, DIAG_NO_STREAM, DIAG_FORCE_STREAM = 64, 128, 512, 1024
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
-INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N = 1, 2, 3, 4, 5
+INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N, INFO_LAST_WEIGH_PASS = 1, 2, 3, 4, 5, 6
+WEIGH_BLOCKS, WEIGH_STREAM = 0, 1
 K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)
 
 # every symbol include/pfmpe.h declares (tests check the .so exports all of them)

@@ -80,6 +80,7 @@ struct pfmpe_ctx {
   int64_t clean_since_fallback = 0;
   int64_t wait_bound_us = 2000000; // PFMPE_OPT_WAIT_BOUND_US: bound of every in-launch wait
   int last_shape = -1;             // PFMPE_SHAPE_* of the last frame
+  int last_weigh_pass = -1;        // PFMPE_WEIGH_* of the last two-launch weighing launch
   int64_t guard_skips = 0;         // one-launch frames run as two launches because another was in flight
   std::map<std::pair<const void*, size_t>, int> occ;  // (kernel, LDS bytes) -> blocks per CU
   Ctrl* d_ctrl = nullptr;
@@ -275,6 +276,7 @@ struct Seq {
     // the extra launches cost more than the prefetch saves; beyond one tile (C4, 611 groups) the separate
     // group / top launches take back what the weighing saves.
     const bool stream = !(c->diag & kDiagNoStream) && ((c->diag & kDiagForceStream) || (MAXM <= 8 && fa.ngrp <= 64));
+    c->last_weigh_pass = stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS;
     if (stream) {
       const void* fn = c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
                                 : (const void*)k_weigh_stream<T, RNG, MAXM, false, SP>;

@@ -664,6 +664,7 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case PFMPE_INFO_FUSED: *value = c->fused; return PFMPE_OK;
     case PFMPE_INFO_FUSED_FALLBACKS: *value = c->fused_fallbacks; return PFMPE_OK;
     case PFMPE_INFO_LAST_SHAPE: *value = c->last_shape; return PFMPE_OK;
+    case PFMPE_INFO_LAST_WEIGH_PASS: *value = c->last_weigh_pass; return PFMPE_OK;
     case PFMPE_INFO_GUARD_SKIPS: *value = c->guard_skips; return PFMPE_OK;
     case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
     default: return PFMPE_E_ARG;

@@ -255,6 +255,8 @@ def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy):
                 snap["counts"] = eng.get_counts()
             snaps.append(snap)
         assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+        assert eng.info(pf.INFO_LAST_WEIGH_PASS) == (pf.WEIGH_STREAM if diag == pf.DIAG_FORCE_STREAM
+                                                     else pf.WEIGH_BLOCKS)
         eng.close()
         res.append(snaps)
     assert res[0][1]["out"]["iters"] == 80
