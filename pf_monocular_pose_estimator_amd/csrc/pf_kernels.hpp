@@ -2196,8 +2196,11 @@ __device__ __forceinline__ void resample_phase(
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, RecOut* __restrict__ out, int32_t seq,
-    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk) {
+    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk, const SP* raw_in = nullptr) {
   constexpr bool INLAUNCH = MODE != 0;
+  // fp16 stored set (RAW): the wave stages its kept particles' stored values as they are (12 halves, 24 B a
+  // row) and the scatter copies them out unchanged, no widening / narrowing (raw_in: the lane's values)
+  constexpr bool RAWROW = RAW && !std::is_same<T, SP>::value;
   const int N = fa.N;
   const int lane = lane_id(), wv = wave_id();
   const int g = blk / fa.gsz;
@@ -2300,8 +2303,19 @@ __device__ __forceinline__ void resample_phase(
   const int wa = lane_value(a, 0);
   const int we = lane_value(e, 63);
   auto& rows = sh.rows[wv];
+  uint2* rraw = (uint2*)&rows[0];  // RAWROW: three 8-B words per row
+  if constexpr (RAWROW) {
+    uint32_t wd6[6];
 #pragma unroll
-  for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];  // also read by wave 0 for the block candidate
+    for (int j = 0; j < 6; ++j)
+      wd6[j] = (uint32_t)__builtin_bit_cast(uint16_t, raw_in[2 * j]) |
+               ((uint32_t)__builtin_bit_cast(uint16_t, raw_in[2 * j + 1]) << 16);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) rraw[3 * lane + j] = make_uint2(wd6[2 * j], wd6[2 * j + 1]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];  // also read by wave 0 for the block candidate
+  }
   if (we > wa) {
     int* map = sh.map[wv];
     int carry = -1;
@@ -2319,10 +2333,21 @@ __device__ __forceinline__ void resample_phase(
       const int k = base + lane;
       wave_lds_sync();  // rows (before the loop) and this chunk's map reads are done before the next clear
       if (k < we) {
-        const auto& row = rows[own];
         SP v[12];
+        if constexpr (RAWROW) {
 #pragma unroll
-        for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+          for (int j = 0; j < 3; ++j) {
+            const uint2 x = rraw[3 * own + j];
+            v[4 * j + 0] = __builtin_bit_cast(SP, (uint16_t)(x.x & 0xffffu));
+            v[4 * j + 1] = __builtin_bit_cast(SP, (uint16_t)(x.x >> 16));
+            v[4 * j + 2] = __builtin_bit_cast(SP, (uint16_t)(x.y & 0xffffu));
+            v[4 * j + 3] = __builtin_bit_cast(SP, (uint16_t)(x.y >> 16));
+          }
+        } else {
+          const auto& row = rows[own];
+#pragma unroll
+          for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+        }
         store_state_raw<SP>(post, fa.ld, k, v);
       }
     }
@@ -2451,13 +2476,15 @@ __device__ __forceinline__ void resample_block(
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
+  SP V[12];  // the kept iteration's stored propagated values (prop0)
   if (prop0) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
     const SP* src = c.kept_slot ? prop1 : prop0;
-    if (valid) {
-      SP v[12];
-      load_state_raw<SP>(src, fa.ld, n, v);
 #pragma unroll
-      for (int q = 0; q < 12; ++q) A[q] = (T)v[q];  // exact (fp16 -> fp32 widening)
+    for (int q = 0; q < 12; ++q) V[q] = SP(0.0f);
+    if (valid) load_state_raw<SP>(src, fa.ld, n, V);
+    if constexpr (std::is_same<T, SP>::value) {  // fp16 rows are staged as they are (resample_phase RAWROW)
+#pragma unroll
+      for (int q = 0; q < 12; ++q) A[q] = V[q];
     }
   }
   stage_consts_from(fa_words, sc);  // visible after block_incl_sum's barrier
@@ -2468,7 +2495,7 @@ __device__ __forceinline__ void resample_block(
   if (prop0)
     resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
                                               cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps,
-                                              nullptr, blk);
+                                              nullptr, blk, V);
   else
     resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
                                         mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk);
