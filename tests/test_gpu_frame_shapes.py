@@ -222,21 +222,24 @@ def test_c4_full_size_properties():
     _full_size_properties("C4", pf.STATE_F16, 0.002)
 
 
-@pytest.mark.parametrize("state,N,M,B,heavy", [(pf.STATE_F64, 140_000, 5, 50, False),
-                                               (pf.STATE_F32, 1_200_000, 5, 50, False),
-                                               (pf.STATE_F16, 1_200_000, 12, 200, True)])
-def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy):
+@pytest.mark.parametrize("state,N,M,B,heavy,rng,prune", [
+    (pf.STATE_F64, 140_000, 5, 50, False, pf.RNG_PHILOX, True),
+    (pf.STATE_F32, 1_200_000, 5, 50, False, pf.RNG_PHILOX, True),
+    (pf.STATE_F16, 1_200_000, 12, 200, True, pf.RNG_PHILOX, True),
+    (pf.STATE_F32, 300_000, 5, 50, False, pf.RNG_REFERENCE, False),  # reference stream, unpruned scan
+])
+def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy, rng, prune):
     """The two-launch path's streaming weighing pass (k_weigh_stream + k_group + k_top: resident blocks
     looping over the 256-particle blocks, the next particle's state prefetched) against the
     one-block-per-256-particles k_propagate_weigh: identical records, weights, propagated and resampled sets
     over a steady frame and an 80-iteration frame (one LED hidden), one tile of groups (140k) and several
-    (1.2M: 4,688 blocks in 74 groups), fp64 / fp32 / fp16 state."""
+    (1.2M: 4,688 blocks in 74 groups), fp64 / fp32 / fp16 state, both RNG streams, pruned and unpruned."""
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 2)
     prior = st.prior(fast=True)
     res = []
     for diag in (pf.DIAG_FORCE_STREAM, pf.DIAG_NO_STREAM):
-        eng = make_engine(N, st.markers, st.K, state, pf.RNG_PHILOX, fused=0)
+        eng = make_engine(N, st.markers, st.K, state, rng, prune=prune, fused=0)
         eng.set_option(pf.OPT_DIAG, diag)
         eng.set_prior(prior)
         snaps = []
