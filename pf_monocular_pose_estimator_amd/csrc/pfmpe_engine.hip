@@ -221,7 +221,6 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_cand, (size_t)c->max_blk * sizeof(Cand)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_mlpose, 12 * sizeof(double)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_flat, kFlatWords * sizeof(uint32_t)) == hipSuccess;
-  ok = ok && hipMemset(c->d_gen, 0, sizeof(uint32_t)) == hipSuccess;
   {
     int coop = 0;
     ok = ok && hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess;
@@ -237,12 +236,18 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_table, table_bytes(c, kMaxBlobs)) == hipSuccess;
   ok &= hipHostMalloc((void**)&c->h_table, table_bytes(c, kMaxBlobs), hipHostMallocDefault) == hipSuccess;
   if (!ok) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_ctrl, 0, sizeof(Ctrl)) != hipSuccess) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand)) != hipSuccess) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_counters, 0, counters_bytes(c)) != hipSuccess) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_flat, 0, kFlatWords * sizeof(uint32_t)) != hipSuccess) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_state[0], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
-  if (hipMemset(c->d_state[1], 0, state_bytes) != hipSuccess) return bad(PFMPE_E_HIP);
+  // Zeroed in the context's own stream and waited for: the stream is non-blocking, so a null-stream
+  // hipMemset could still be in flight when the first frame's kernels read these words (freed memory of an
+  // earlier context: a stale control record, counters or candidate tags).
+  ok = ok && hipMemsetAsync(c->d_gen, 0, sizeof(uint32_t), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_state[0], 0, state_bytes, c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_state[1], 0, state_bytes, c->stream) == hipSuccess;
+  ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+  if (!ok) return bad(PFMPE_E_HIP);
   *out = c;
   return PFMPE_OK;
 }
@@ -322,7 +327,8 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       if ((c->diag & kDiagStamps) && !c->d_stamps) {
         RET(set_device(c));
         HIPCHK(c, hipMalloc((void**)&c->d_stamps, (1 + (size_t)c->max_blk) * kStamps * sizeof(uint64_t)));
-        HIPCHK(c, hipMemset(c->d_stamps, 0, (1 + (size_t)c->max_blk) * kStamps * sizeof(uint64_t)));
+        HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, (1 + (size_t)c->max_blk) * kStamps * sizeof(uint64_t), c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
       }
       return PFMPE_OK;
     default:
@@ -384,7 +390,8 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
   for (int f = 0; f < nframes; ++f)
     build_table(c, blobs + 2 * (size_t)offsets[f], c->bank_B[f], host.data() + c->bank_off[f]);
   HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
-  HIPCHK(c, hipMemcpy(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice));
+  HIPCHK(c, hipMemcpyAsync(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // `host` goes out of scope; the frames read the bank in this stream
   return PFMPE_OK;
 }
 
@@ -621,7 +628,9 @@ int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
   if (!c->record_counts || !c->d_counts) return fail(c, PFMPE_E_STATE, "get_counts: PFMPE_OPT_RECORD_COUNTS off");
   if (!c->has_last || !c->last_accepted) return fail(c, PFMPE_E_STATE, "get_counts: last step did not resample");
   RET(set_device(c));
-  HIPCHK(c, hipMemcpy(out, c->d_counts, (size_t)c->N * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  // in the context's stream: the frame's kernel may still be retiring after its record reached the host
+  HIPCHK(c, hipMemcpyAsync(out, c->d_counts, (size_t)c->N * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   return PFMPE_OK;
 }
 
@@ -631,13 +640,13 @@ int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
   RET(set_device(c));
   const size_t rows = 1 + (size_t)c->max_blk;
   if (!out) {
+    HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, rows * kStamps * sizeof(uint64_t), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemset(c->d_stamps, 0, rows * kStamps * sizeof(uint64_t)));
     return PFMPE_OK;
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
   std::vector<uint64_t> h(rows * kStamps);
-  HIPCHK(c, hipMemcpy(h.data(), c->d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   for (int i = 0; i < kStamps; ++i) {
     const bool is_min = i == 0 || i == 4 || i == 19;
     uint64_t v = h[i];
