@@ -79,6 +79,7 @@ struct FrameArgsT {
   int32_t ngrp, gsz;              // reduction groups and blocks per group (~sqrt(nblk), <= kGroup)
   int32_t diag;                   // diagnostic switches (0 in production; pfmpe_ctx.hpp kDiag*)
   int32_t small_angles;           // every angle draw of the frame has |x| <= kSmallAngle (host bound, fp32)
+  int32_t k_upper;                // K = [k0 k1 k2; 0 k4 k5; 0 0 1] (host check; fp32 skips the zero terms)
   uint32_t wait_ticks;            // bound of every in-launch wait, s_memrealtime ticks (100 MHz)
   uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
   int64_t ld;                     // SoA plane stride in elements
@@ -440,11 +441,23 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const Lds
   propagate<T, RNG>(fa, sc, A, n, iter, P);
 }
 
-// project2d (PE:1017-1034): p = (K34*T) * [X;1], u = p/p.z — full K, no distortion, no z>0 test
-template <typename T, int MAXM>
-__device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* P, T* u,
-                                                T* v) {
-  T Q[12];
+// Q = K * P (3x4).  fp32 with an upper-triangular K whose last row is (0 0 1) (every pinhole CameraInfo,
+// README.md:95-143; the host checks, FrameArgsT::k_upper): the zero terms are skipped, 16 instead of 36
+// operations.  A skipped term is an exact +-0 added before the first rounding, so the sums are the same
+// except for the sign of an exact zero.  fp64 (the parity mode) keeps the literal form.
+template <typename T>
+__device__ __forceinline__ void k_times_pose(const LdsConst<T>& sc, const T* P, bool k_upper, T* Q) {
+  if (std::is_same<T, float>::value && k_upper) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      T s = sc.K[0] * P[0 * 4 + j];
+      s = fmadd(sc.K[1], P[1 * 4 + j], s);
+      Q[0 * 4 + j] = fmadd(sc.K[2], P[2 * 4 + j], s);
+      Q[1 * 4 + j] = fmadd(sc.K[5], P[2 * 4 + j], sc.K[4] * P[1 * 4 + j]);
+      Q[2 * 4 + j] = P[2 * 4 + j];
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
 #pragma unroll
@@ -455,6 +468,14 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
       Q[i * 4 + j] = s;
     }
   }
+}
+
+// project2d (PE:1017-1034): p = (K34*T) * [X;1], u = p/p.z — full K, no distortion, no z>0 test
+template <typename T, int MAXM>
+__device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const T* P, T* u,
+                                                T* v) {
+  T Q[12];
+  k_times_pose<T>(sc, P, fa.k_upper != 0, Q);
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     if (j < fa.M) {
@@ -477,18 +498,9 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
 // project_markers' arithmetic for ONE marker j (wave-uniform index): the same operation order, so the
 // same bits
 template <typename T>
-__device__ __forceinline__ void project_one(const LdsConst<T>& sc, const T* P, int j, T& u, T& v) {
+__device__ __forceinline__ void project_one(const LdsConst<T>& sc, const T* P, int j, bool k_upper, T& u, T& v) {
   T Q[12];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      T s = sc.K[i * 3 + 0] * P[0 * 4 + c];
-      s = fmadd(sc.K[i * 3 + 1], P[1 * 4 + c], s);
-      s = fmadd(sc.K[i * 3 + 2], P[2 * 4 + c], s);
-      Q[i * 4 + c] = s;
-    }
-  }
+  k_times_pose<T>(sc, P, k_upper, Q);
   const T X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
   T p[3];
 #pragma unroll
@@ -2618,7 +2630,7 @@ __device__ __forceinline__ void resample_final_block(
     make_particle<T, RNG, SP>(fa, sc, prior, bi, c.kept_iter, Pc);
   }
   // wave j: marker j's nearest blob (pose_pairs' scan and tie rule, one marker per wave)
-  project_one<T>(sc, Pc, wv, u0, v0);
+  project_one<T>(sc, Pc, wv, fa.k_upper != 0, u0, v0);
   T best = inf_t<T>();
   int arg = 0x7fffffff;
   for (int i = lane; i < fa.B; i += 64) {

@@ -739,6 +739,7 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
     for (int q = 0; q < 3; ++q) amax = std::max(amax, std::max(std::abs(fa.dlo[q]), std::abs(fa.dhi[q])));
     fa.small_angles = (sizeof(T) == 4 && amax * std::abs(gmax) <= 0.999 * (double)kSmallAngle) ? 1 : 0;
   }
+  fa.k_upper = (fa.K[3] == (T)0 && fa.K[6] == (T)0 && fa.K[7] == (T)0 && fa.K[8] == (T)1) ? 1 : 0;
   fa.tol = (T)p.tol;
   fa.tol_pf = (T)p.tol_pf;
   // every blob with sqrt(d2) <= tol_pf (in T arithmetic) has |dx| <= tolq
