@@ -1015,8 +1015,11 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   if (!(x >= 0.0)) return 0;  // r_k >= 0; also -inf / NaN
   const double xn = x * (double)N;
   const double fk = floor(xn);
+  // the neighbour scans run almost never: kept as rolled loops (no unroll, no interleave), so their inlined
+  // RNG copies add less scalar register pressure (static SGPR spills of k_resample 557 -> 293)
   if (!(fk < (double)N)) {  // x >= ~1: scan down from N
     int64_t k = N;
+#pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
     while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
     return k;
   }
@@ -1024,9 +1027,12 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   const double f = xn - fk;
   if (target_r<T, RNG>(fa, iters, k) <= x) {
     ++k;
-    if (1.0 - f <= kEdge)
+    if (1.0 - f <= kEdge) {
+#pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
       while (k < N && target_r<T, RNG>(fa, iters, k) <= x) ++k;
+    }
   } else if (f <= kEdge) {
+#pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
     while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
   }
   return k;
