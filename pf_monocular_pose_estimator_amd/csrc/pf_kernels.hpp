@@ -982,8 +982,9 @@ __device__ __forceinline__ void bcast63(V& v, int& i) {
 
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
+// fl(k + U_k): the numerator of target r_k = fl(fl(k + U_k) / N)
 template <typename T, int RNG>
-__device__ __forceinline__ double target_r(const FrameArgsT<T>& fa, int iters, int64_t k) {
+__device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters, int64_t k) {
   double U;
   if (RNG == kRngReference) {
     const uint64_t motion = fa.N > 2 ? (uint64_t)12 * (uint64_t)(fa.N - 2) * (uint64_t)iters : 0u;
@@ -994,7 +995,24 @@ __device__ __forceinline__ double target_r(const FrameArgsT<T>& fa, int iters, i
     const U32x4 o = philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
     U = u53(o.x, o.y);
   }
-  return ((double)k + U) / (double)fa.N;
+  return (double)k + U;
+}
+
+// r_k <= x, decided exactly without the fp64 division in all but a vanishing band.  With a = fl(k + U_k) and
+// the exact real residual x*N - a, whose sign the single rounding of fma(x, N, -a) preserves:
+//   x*N - a >= 0  ->  a/N <= x  ->  fl(a/N) <= x (rounding is monotone and x is a double);
+//   a - x*N > N*ulp(x)  ->  a/N > x + ulp(x)  ->  fl(a/N) > x.
+// thr = fl(x*N)*2^-50 + 2^-1000 bounds N*ulp(x) from above with a wide margin (ulp(x) <= x*2^-52 for normal x;
+// the absolute term covers tiny x).  Between the two (a within ~2^-50 relative of x*N) the reference's own
+// division decides.  xn = fl(x*N), thr = fma(xn, 2^-50, 2^-1000): per call site, computed once.
+template <typename T, int RNG>
+__device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, int64_t k, double x, double thr) {
+  const double a = target_num<T, RNG>(fa, iters, k);
+  const double Nd = (double)fa.N;
+  const double e = __builtin_fma(x, Nd, -a);
+  if (e >= 0.0) return true;
+  if (-e > thr) return false;
+  return a / Nd <= x;  // the reference's rounding (PE:674-679 compares the divided target)
 }
 
 // F(x) = #{k : r_k <= x}.  r_k is non-decreasing in k, so target k finds the first particle i whose
@@ -1017,23 +1035,24 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   const double fk = floor(xn);
   // the neighbour scans run almost never: kept as rolled loops (no unroll, no interleave), so their inlined
   // RNG copies add less scalar register pressure (static SGPR spills of k_resample 557 -> 293)
+  const double thr = __builtin_fma(xn, 0x1p-50, 0x1p-1000);  // target_le's band (xn = +inf: never reached)
   if (!(fk < (double)N)) {  // x >= ~1: scan down from N
     int64_t k = N;
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
+    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
     return k;
   }
   int64_t k = (int64_t)fk;
   const double f = xn - fk;
-  if (target_r<T, RNG>(fa, iters, k) <= x) {
+  if (target_le<T, RNG>(fa, iters, k, x, thr)) {
     ++k;
     if (1.0 - f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-      while (k < N && target_r<T, RNG>(fa, iters, k) <= x) ++k;
+      while (k < N && target_le<T, RNG>(fa, iters, k, x, thr)) ++k;
     }
   } else if (f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && target_r<T, RNG>(fa, iters, k - 1) > x) --k;
+    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
   }
   return k;
 }

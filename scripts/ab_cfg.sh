@@ -11,7 +11,7 @@ for cfg in ${CONFIGS:-C4 C3 C2}; do
   for r in 1 2 3; do
     for v in base new; do
       if [ $v = base ]; then export PFMPE_LIB_OVERRIDE=$PWD/ab/libpfmpe_base.so; else unset PFMPE_LIB_OVERRIDE; fi
-      timeout -k 10 300 python bench.py --config $cfg --cpu-frames 0 --steps $st --warmup 5 > gpurun_out/ab_$v.log 2>&1 || { tail gpurun_out/ab_$v.log; exit 1; }
+      timeout -k 10 300 python bench.py --config $cfg --cpu-frames 0 --steps $st --warmup 5 ${AB_EXTRA} > gpurun_out/ab_$v.log 2>&1 || { tail gpurun_out/ab_$v.log; exit 1; }
       python3 -c "import json; d=json.load(open('gpurun_out/ab_$v.log')); print('$cfg $v', round(d['ms_per_step']*1e3,2), 'us/frame', d['roofline']['per_kernel_avg_us'])"
     done
   done
