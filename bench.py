@@ -73,6 +73,10 @@ def parse():
                     help="after the timed region, also run S independent streams of the config per GPU as one "
                          "batch (pfmpe_step_multi) for each S in this comma list; default 1,4,8,16 at C2 on one GPU")
     ap.add_argument("--multi-steps", type=int, default=50, help="timed batches per multi-stream point")
+    ap.add_argument("--multi-groups", default="1,2",
+                    help="batches per multi-stream point, each on its own host thread and HIP stream (comma list)")
+    ap.add_argument("--scale-ref-steps", type=int, default=100,
+                    help="frames of the one-GPU C5 reference beside the default C2 line (0 = skip)")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
     return ap.parse_args()
@@ -224,10 +228,13 @@ def occluded_frames(eng, st, rank: int, n: int, first_index: int):
 
 
 def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dtype: int, rng: int, device: int,
-                       sid0: int, prune: int, keep_prop: int):
+                       sid0: int, prune: int, keep_prop: int, groups: int = 1):
     """S independent streams of `base` on one GPU, each frame of all S run as ONE batch (pfmpe_step_multi:
     one weighing launch over every stream's blocks, one resampling launch, one finishing launch).  Blob tables
-    come from each stream's staged bank; the timed loop is pfmpe_step_multi_batch (the C loop a tracker runs)."""
+    come from each stream's staged bank; the timed loop is pfmpe_step_multi_batch (the C loop a tracker runs).
+    groups > 1: the streams split into that many batches, each driven by its own host thread on its own HIP
+    stream (ctypes releases the GIL in the C loop), so one batch's host turnaround (record wait, descriptor
+    staging, launch) overlaps the other batches' kernels."""
     import ctypes as C
     engs, frames = [], []
     n = warmup + steps
@@ -248,26 +255,83 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
             frames.append([eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs),
                                           bank_frame=f.index, dt=f.dt, seed=((1000 * sid0 + s) << 32) + 17 + f.index,
                                           frame_idx=f.index) for f in st.frames])
+        import threading
         lib = engs[0].lib
-        ctxs = (C.c_void_p * S)(*[e.ctx.value for e in engs])
-        ins = (pf.FrameIn * (S * n))(*[frames[s][f] for f in range(n) for s in range(S)])  # batch-major
-        outs = (pf.FrameOut * (S * n))()
-        done = C.c_int()
         fin, fout = C.sizeof(pf.FrameIn), C.sizeof(pf.FrameOut)
-        at_in = lambda f: C.cast(C.byref(ins, f * S * fin), C.POINTER(pf.FrameIn))  # noqa: E731
-        at_out = lambda f: C.cast(C.byref(outs, f * S * fout), C.POINTER(pf.FrameOut))  # noqa: E731
-        engs[0]._chk(lib.pfmpe_step_multi_batch(ctxs, S, at_in(0), warmup, at_out(0), C.byref(done)))
+        G = max(1, min(groups, S))
+        parts = [list(range(S))[g::G] for g in range(G)]
+        runs = []
+        for part in parts:
+            Sg = len(part)
+            ctxs = (C.c_void_p * Sg)(*[engs[s].ctx.value for s in part])
+            ins = (pf.FrameIn * (Sg * n))(*[frames[s][f] for f in range(n) for s in part])  # batch-major
+            outs = (pf.FrameOut * (Sg * n))()
+            runs.append((Sg, ctxs, ins, outs, engs[part[0]]))
+
+        def drive(r, first, count, errs):
+            Sg, ctxs, ins, outs, e0 = r
+            done = C.c_int()
+            pin = C.cast(C.byref(ins, first * Sg * fin), C.POINTER(pf.FrameIn))
+            pout = C.cast(C.byref(outs, first * Sg * fout), C.POINTER(pf.FrameOut))
+            rc = lib.pfmpe_step_multi_batch(ctxs, Sg, pin, count, pout, C.byref(done))
+            if rc != 0:
+                errs.append(e0.ctx)
+                e0._chk(rc)
+
+        def run_all(first, count):
+            errs = []
+            if G == 1:
+                drive(runs[0], first, count, errs)
+                return
+            th = [threading.Thread(target=drive, args=(r, first, count, errs)) for r in runs]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errs:
+                raise RuntimeError("pfmpe_step_multi_batch failed in a batch thread")
+
+        run_all(0, warmup)
         t0 = time.perf_counter()  # the C loop a multi-object tracker runs: every batch blocks on its records
-        engs[0]._chk(lib.pfmpe_step_multi_batch(ctxs, S, at_in(warmup), steps, at_out(warmup), C.byref(done)))
+        run_all(warmup, steps)
         el = time.perf_counter() - t0
-        upd = sum(base.N * outs[i].iters for i in range(warmup * S, n * S))
-        acc = sum(outs[i].accepted for i in range(warmup * S, n * S))
-        return {"streams": S, "N_per_stream": base.N, "live_particles": S * base.N,
+        upd = sum(base.N * r[3][i].iters for r in runs for i in range(warmup * r[0], n * r[0]))
+        acc = sum(r[3][i].accepted for r in runs for i in range(warmup * r[0], n * r[0]))
+        return {"streams": S, "groups": G, "N_per_stream": base.N, "live_particles": S * base.N,
                 "updates_per_s": upd / el, "ms_per_batch": el * 1e3 / steps,
                 "frames_per_sec_per_stream": steps / el, "accept_rate": acc / (S * steps)}
     finally:
         for e in engs:
             e.close()
+
+
+def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args):
+    """One stream of `base` (f32 state) on one GPU, timed as the main line is (pfmpe_step_batch: every frame
+    blocks on its record)."""
+    cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
+    st = syn.make_stream(cfg, warmup + steps)
+    eng = pf.Engine(device=device, max_particles=cfg.N, state_dtype=pf.STATE_F32)
+    try:
+        eng.set_model(st.markers, st.K)
+        prm = pf.default_params()
+        prm.rng_mode = rng
+        eng.set_params(prm)
+        eng.set_prior(st.prior())
+        eng.set_option(pf.OPT_FUSED, args.fused)
+        eng.set_option(pf.OPT_PRUNE, args.prune)
+        eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
+        eng.stage_blob_bank([f.blobs for f in st.frames])
+        frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
+                                 dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index) for f in st.frames]
+        for f in frames[:warmup]:
+            eng.step(f)
+        t0 = time.perf_counter()
+        outs = eng.step_batch(frames[warmup:])
+        el = time.perf_counter() - t0
+        return {"value": sum(cfg.N * o.iters for o in outs) / el, "unit": "particle-updates/s",
+                "ms_per_frame": el * 1e3 / steps, "frames": steps}
+    finally:
+        eng.close()
 
 
 def main():
@@ -364,13 +428,27 @@ def main():
     sweep = args.multi_sweep or ("1,4,8,16" if world == 1 and config == "C2" and not args.occlude else "")
     if sweep and rank == 0:  # untimed by the driver's contract: reported beside the line
         Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
-        multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi); "
+        multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi), "
+                         "split into `groups` concurrent batches (one host thread and HIP stream each); "
                          "frac = updates/s x (3S+8) B / 8 TB/s", "points": []}
+        gsweep = [int(x) for x in args.multi_groups.split(",") if x]
         for S_ in [int(x) for x in sweep.split(",") if x]:
-            pt = multi_stream_point(pf, syn, base, S_, args.multi_steps, 5, state_dtype, prm.rng_mode, device, sid,
-                                    args.prune, args.keep_prop)
-            pt["frac"] = round(pt["updates_per_s"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
-            multi["points"].append(pt)
+            for G_ in gsweep:
+                if G_ > 1 and S_ < 2 * G_:
+                    continue
+                pt = multi_stream_point(pf, syn, base, S_, args.multi_steps, 5, state_dtype, prm.rng_mode, device,
+                                        sid, args.prune, args.keep_prop, G_)
+                pt["frac"] = round(pt["updates_per_s"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
+                multi["points"].append(pt)
+
+    scale_ref = None
+    if world == 1 and config == "C2" and not args.config and not args.occlude and args.scale_ref_steps > 0:
+        # the per-GPU workload of the --gpus N > 1 lines (one C5 stream per GPU) on this one GPU, so the
+        # N = 1 point of a scaling curve exists for the same workload (untimed by the driver's contract)
+        scale_ref = single_stream_point(pf, syn, syn.CONFIGS["C5"], args.scale_ref_steps, 10, prm.rng_mode, device,
+                                        sid, args)
+        scale_ref["what"] = ("one C5 stream (BASELINE.json configs[4]: M=5, B=50, N=1M, f32) on this GPU, timed like "
+                             "the main line: the per-GPU workload of bench.py --gpus N > 1, for its N = 1 point")
 
     if rank == 0:
         S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
@@ -436,6 +514,7 @@ def main():
             "cpu_baseline": cpu,
             "worst_case": worst,
             "multi_stream": multi,
+            "scaling_reference": scale_ref,
         }
         print(json.dumps(line), flush=True)
     eng.close()
