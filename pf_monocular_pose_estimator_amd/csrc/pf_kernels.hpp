@@ -1907,8 +1907,11 @@ __device__ __forceinline__ void propagate_weigh_block(
                             ctrl, gcount, tcount, nullptr, 0u, stamps, blk);
 }
 
+#ifndef PFMPE_WEIGH_MIN_WAVES
+#define PFMPE_WEIGH_MIN_WAVES 1
+#endif
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) void k_propagate_weigh(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_MIN_WAVES))) void k_propagate_weigh(
     const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior, T* __restrict__ w0,
     T* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
     BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
@@ -2538,8 +2541,15 @@ __device__ __forceinline__ void resample_block(
                                         mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk);
 }
 
+// Occupancy floor of k_resample / k_resample_multi (waves per SIMD; 1 = the compiler's choice).  Unconstrained
+// the fp16-state k_resample takes 85 VGPRs (5 waves); the fp16 TUs set 7 (72 VGPRs, a few rarely-live values
+// spilled): at C4 (10M particles) 196 -> 170 us, the kernel being latency bound.  The fp32 TUs
+// set 6 (batched 16-32 x C2 / C5 +2-3 %).  8 waves spill 78 VGPRs.
+#ifndef PFMPE_RESAMPLE_MIN_WAVES
+#define PFMPE_RESAMPLE_MIN_WAVES 1
+#endif
 template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kBlock) void k_resample(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_MIN_WAVES))) void k_resample(
     const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
     SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
@@ -2555,7 +2565,8 @@ __global__ __launch_bounds__(kBlock) void k_resample(
 }
 
 template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kBlock) void k_resample_multi(const StreamDesc<T, SP>* __restrict__ descs,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_MIN_WAVES))) void k_resample_multi(
+    const StreamDesc<T, SP>* __restrict__ descs,
                                                            const uint16_t* __restrict__ bmap) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;

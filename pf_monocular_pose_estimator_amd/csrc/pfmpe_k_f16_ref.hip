@@ -1,4 +1,7 @@
 // pfmpe_k_f16_ref.hip — kernel instantiations for fp16-delta state (fp32 compute), kRngReference.
+#ifndef PFMPE_RESAMPLE_MIN_WAVES
+#define PFMPE_RESAMPLE_MIN_WAVES 7  // k_resample: 7 waves per SIMD (pf_kernels.hpp)
+#endif
 #include "pfmpe_ctx.hpp"
 
 namespace pfmpe_impl {

@@ -1,4 +1,7 @@
 // pfmpe_k_f32_philox.hip — kernel instantiations for float state, kRngPhilox (one TU per pair: parallel build).
+#ifndef PFMPE_RESAMPLE_MIN_WAVES
+#define PFMPE_RESAMPLE_MIN_WAVES 6  // k_resample / k_resample_multi: 6 waves per SIMD (pf_kernels.hpp)
+#endif
 #include "pfmpe_ctx.hpp"
 
 namespace pfmpe_impl {
