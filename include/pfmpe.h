@@ -334,7 +334,7 @@ enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 aft
        PFMPE_INFO_LAST_WEIGH_PASS = 6 };/* PFMPE_WEIGH_* of the last two-launch weighing (-1: none)  */
 /* The two-launch shape's weighing pass: one block per 256 particles (k_propagate_weigh), or
  * resident blocks streaming over them with the next block's state prefetched (k_weigh_stream + k_group +
- * k_top; chosen for <= 8 markers and <= 64 block groups).  Both give bit-identical results. */
+ * k_top; chosen for <= 8 markers).  Both give bit-identical results. */
 enum { PFMPE_WEIGH_BLOCKS = 0, PFMPE_WEIGH_STREAM = 1 };
 int pfmpe_get_info(const pfmpe_ctx* ctx, int key, int64_t* value);
 

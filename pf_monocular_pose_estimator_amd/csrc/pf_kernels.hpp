@@ -1721,8 +1721,13 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
 // the block partials are plain stores read by k_group_top after the launch boundary (no arrival counters,
 // no group / top tail in this launch).  Per 256-particle block the arithmetic and the partial are exactly
 // k_propagate_weigh's, so the weights, partials and every later decision are bit-identical.
+// Occupancy floor of k_weigh_stream (waves per SIMD; 1 = the compiler's choice): the fp16 TUs set 6 (85 -> 80
+// VGPRs: C4 weighing 241 -> 233 us); 7 was slower at C4 and C5.
+#ifndef PFMPE_WEIGH_STREAM_MIN_WAVES
+#define PFMPE_WEIGH_STREAM_MIN_WAVES 1
+#endif
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) void k_weigh_stream(const FrameArgsT<T> fa, const unsigned char* __restrict__ table,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_STREAM_MIN_WAVES))) void k_weigh_stream(const FrameArgsT<T> fa, const unsigned char* __restrict__ table,
                                                          const SP* __restrict__ prior, T* __restrict__ w0,
                                                          T* __restrict__ w1, BlockPart* __restrict__ part0,
                                                          BlockPart* __restrict__ part1, const Ctrl* __restrict__ ctrl,

@@ -306,12 +306,11 @@ struct Seq {
     SP* prop0 = c->keep_prop ? (SP*)c->d_prop[0] : nullptr;
     SP* prop1 = c->keep_prop ? (SP*)c->d_prop[1] : nullptr;
     // The streaming weighing pass (k_weigh_stream: resident blocks looping over the 256-particle blocks, the
-    // next particle's state prefetched) with the group / top hand-off as two small launches.  It wins where
-    // the weighing waits on HBM and the top is one tile of groups: <= 8 markers and <= 64 groups (N <= 1M;
-    // C5: 52 -> 31 us weighing, 104 -> 95 us per frame).  At 12 markers (C3) the weighing is VALU bound and
-    // the extra launches cost more than the prefetch saves; beyond one tile (C4, 611 groups) the separate
-    // group / top launches take back what the weighing saves.
-    const bool stream = !(c->diag & kDiagNoStream) && ((c->diag & kDiagForceStream) || (MAXM <= 8 && fa.ngrp <= 64));
+    // next particle's state prefetched) with the group / top hand-off as two small launches.  It wins for
+    // <= 8 markers (C5: 52 -> 31 us weighing, 104 -> 95 us per frame; C4 with the 6-wave fp16 build: weighing
+    // 265 -> 233 us, of which the 611-group hand-off takes back ~21 us).  At 12 markers (C3) the weighing is
+    // VALU bound and the extra launches cost more than the prefetch saves.
+    const bool stream = !(c->diag & kDiagNoStream) && ((c->diag & kDiagForceStream) || MAXM <= 8);
     c->last_weigh_pass = stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS;
     if (stream) {
       const void* fn = c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
