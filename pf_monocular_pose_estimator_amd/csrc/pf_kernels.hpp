@@ -1136,7 +1136,8 @@ enum : int {
   kDiagAbandon = 128,   // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
   kDiagSortedScore = 256, // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
   kDiagNoStream = 512,     // two-launch path: never the streaming weighing pass (k_weigh_stream + k_group + k_top)
-  kDiagForceStream = 1024  // two-launch path: always the streaming weighing pass (tests / A/B)
+  kDiagForceStream = 1024, // two-launch path: always the streaming weighing pass (tests / A/B)
+  kDiagSerialTop = 2048    // streaming pass with > 64 groups: the one-wave k_top instead of k_top_wide (A/B)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -1861,6 +1862,148 @@ __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* _
     staged = gsm;
   }
   propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, nullptr, 0u, g0, single, slot, staged);
+}
+
+// ---- k_top for more than one tile of groups (ngrp > 64, partials staged in LDS): 16 waves instead of one.
+// The per-tile work of propagate_top's final-iteration passes (the tile's inclusive sum, its G_g, the
+// normalised group-start values and their in-tile max scan) runs one tile per wave in parallel; only the
+// carried parts stay serial, in wave 0 and in the same order: S = ((0 + T_0) + T_1) + ... over the tile
+// totals T_t (each the last lane of the tile's wave_incl_sum, as in propagate_top), the carry into tile t,
+// and the running max over earlier tiles (a fold of `tm > run ? tm : run`, which ignores NaN and is the max
+// of the rest: order-free).  So G_g, Gin_g, S, Rmax and the record are bit-identical to propagate_top's.
+// Non-final iterations, and a final iteration whose kept partials are an earlier iteration's (not staged),
+// run propagate_top itself in wave 0.
+constexpr int kTopWaves = 16;
+constexpr int kTopMaxTiles = 24;  // ngrp <= 1365 (staged) -> <= 22 tiles
+template <typename T, int RNG>
+__global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
+                                                          GroupPart* __restrict__ gpart1,
+                                                          GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+                                                          int iter) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries
+  __shared__ double tileT[kTopMaxTiles], tileM[kTopMaxTiles], carryT[kTopMaxTiles];
+  __shared__ double S_sh;
+  __shared__ int wide;
+  if (ctrl->done) return;  // uniform
+  const int slot = ctrl->cur_slot;
+  const GroupPart* src = slot ? gpart1 : gpart0;
+  const int lane = lane_id(), wv = (int)(threadIdx.x >> 6);
+  const int ngrp = fa.ngrp, ntiles = (ngrp + 63) / 64;
+  GroupPart none;
+  none.sum = 0.0;
+  none.zmax = -INFINITY;
+  none.zmin = INFINITY;
+  none.maxw = -INFINITY;
+  none.minw = INFINITY;
+  none.argmax = none.argmin = 0x7fffffff;
+  for (int g = (int)threadIdx.x; g < ngrp; g += 64 * kTopWaves) gsm[g] = group_part(src, g, none, false);
+  __syncthreads();
+  // tile totals of this iteration's group sums (used if this iteration turns out to be the kept one)
+  for (int t = wv; t < ntiles; t += kTopWaves) {
+    const int g = t * 64 + lane;
+    const double incl = wave_incl_sum(g < ngrp ? gsm[g].sum : 0.0);
+    if (lane == 63) tileT[t] = incl;
+  }
+  __syncthreads();
+  Ctrl c;
+  if (wv == 0) {  // propagate_top's head: this iteration's max / first argmax, best, exit rule
+    double mv = -INFINITY;
+    int mi = 0x7fffffff;
+    for (int g = lane; g < ngrp; g += 64) cmb_max(mv, mi, gsm[g].maxw, gsm[g].argmax);
+    wave_argmax(mv, mi);
+    c = load_ctrl_wt(ctrl);
+    if (mv > c.best_max) {  // strict: PE:608
+      c.best_max = mv;
+      c.best_idx = mi;
+      c.best_iter = iter;
+      c.best_slot = slot;
+      c.has_best = 1;
+    }
+    c.iters = iter + 1;
+    const bool go_on = fa.force_iters > 0 ? (c.iters < fa.force_iters)
+                                          : (c.iters < fa.max_iter && mv < fa.exit_thr);  // PE:616
+    const int kept_slot = c.has_best ? c.best_slot : slot;
+    const int w = (!go_on && kept_slot == slot) ? 1 : 0;
+    if (w) {
+      c.cur_slot = c.has_best ? 1 - c.best_slot : 1 - slot;
+      c.done = 1;
+      c.kept_slot = kept_slot;
+      c.kept_iter = c.has_best ? c.best_iter : iter;
+      double carry = 0.0;
+      for (int t = 0; t < ntiles; ++t) {
+        if (lane == 0) carryT[t] = carry;
+        carry = carry + tileT[t];
+      }
+      if (lane == 0) S_sh = carry;
+    } else {
+      propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, nullptr, 0u, none, false, slot, gsm);
+    }
+    if (lane == 0) wide = w;
+  }
+  __syncthreads();
+  if (!wide) return;
+  const double S = S_sh;
+  // per tile: G_g and the normalised group-start values' in-tile max scan (propagate_top's second pass)
+  double exl[(kTopMaxTiles + kTopWaves - 1) / kTopWaves];
+#pragma unroll
+  for (int i = 0; i < (kTopMaxTiles + kTopWaves - 1) / kTopWaves; ++i) {
+    const int t = wv + i * kTopWaves;
+    exl[i] = -INFINITY;
+    if (t < ntiles) {  // wave-uniform
+      const int g = t * 64 + lane;
+      GroupPart q;
+      q.sum = 0.0;
+      q.zmax = -INFINITY;
+      q.zmin = INFINITY;
+      if (g < ngrp) q = gsm[g];
+      const double incl = wave_incl_sum(q.sum);
+      const double prev = wave_shr1(incl, 0.0);
+      const double G = lane == 0 ? carryT[t] : carryT[t] + prev;
+      double cm = -INFINITY;
+      if (g < ngrp && S != 0.0) cm = (G + (S > 0.0 ? q.zmax : q.zmin)) / S;
+      const double im = wave_incl_max(cm);
+      exl[i] = wave_shr1(im, -(double)INFINITY);
+      if (g < ngrp) st_wt_d(&gscan[g].G, G);
+      if (lane == 63) tileM[t] = im;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < (kTopMaxTiles + kTopWaves - 1) / kTopWaves; ++i) {
+    const int t = wv + i * kTopWaves;
+    if (t < ntiles) {
+      double run = -INFINITY;
+      for (int u = 0; u < t; ++u) run = tileM[u] > run ? tileM[u] : run;
+      const double ex = exl[i] > run ? exl[i] : run;
+      const int g = t * 64 + lane;
+      if (g < ngrp) st_wt_d(&gscan[g].Gin, ex);
+    }
+  }
+  if (wv != 0) return;
+  // propagate_top's tail: Rmax, the kept iteration's argmax / argmin, accept, the record
+  double run = -INFINITY;
+  for (int u = 0; u < ntiles; ++u) run = tileM[u] > run ? tileM[u] : run;
+  if (S == 0.0) run = -INFINITY;
+  double amv = -INFINITY, anv = INFINITY;
+  int ami = 0x7fffffff, ani = 0x7fffffff;
+  for (int g = lane; g < ngrp; g += 64) {
+    cmb_max(amv, ami, gsm[g].maxw, gsm[g].argmax);
+    cmb_min(anv, ani, gsm[g].minw, gsm[g].argmin);
+  }
+  wave_argmax(amv, ami);
+  wave_argmin(anv, ani);
+  const double highest = c.has_best ? c.best_max : 0.0;
+  c.S = S;
+  c.Rmax = run;
+  c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
+  if (c.accepted) {
+    c.most_likely_idx = c.best_idx;
+    c.K_total = lane == 0 ? count_targets<T, RNG>(fa, c.iters, run) : 0;
+  } else {
+    c.most_likely_idx = (S < 0.0) ? ani : ami;  // PE:714
+    c.K_total = 0;
+  }
+  if (lane == 0) store_ctrl_wt(ctrl, c);
 }
 
 // ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread.

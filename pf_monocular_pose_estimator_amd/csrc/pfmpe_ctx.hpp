@@ -339,8 +339,12 @@ struct Seq {
       return launch_ext(c, PFMPE_K_AUX, [&] {
         klaunch(c, k_group<T>, dim3(fa.ngrp), dim3(64), 0, fa, c->d_part[0], c->d_part[1],
                            c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], (const Ctrl*)c->d_ctrl);
-        klaunch(c, k_top<T, RNG>, dim3(1), dim3(64), staged ? glds : 0, fa, c->d_gpart[0],
-                           c->d_gpart[1], c->d_gscan, c->d_ctrl, iter, staged ? 1 : 0);
+        if (staged && fa.ngrp <= 64 * kTopMaxTiles && !(c->diag & kDiagSerialTop))  // > 1 tile: k_top_wide
+          klaunch(c, k_top_wide<T, RNG>, dim3(1), dim3(64 * kTopWaves), glds, fa, c->d_gpart[0], c->d_gpart[1],
+                  c->d_gscan, c->d_ctrl, iter);
+        else
+          klaunch(c, k_top<T, RNG>, dim3(1), dim3(64), staged ? glds : 0, fa, c->d_gpart[0],
+                             c->d_gpart[1], c->d_gscan, c->d_ctrl, iter, staged ? 1 : 0);
       });
     }
     return launch_ext(c, PFMPE_K_PROPAGATE, [&] {

@@ -227,13 +227,17 @@ def test_c4_full_size_properties():
     (pf.STATE_F32, 1_200_000, 5, 50, False, pf.RNG_PHILOX, True),
     (pf.STATE_F16, 1_200_000, 12, 200, True, pf.RNG_PHILOX, True),
     (pf.STATE_F32, 300_000, 5, 50, False, pf.RNG_REFERENCE, False),  # reference stream, unpruned scan
+    (pf.STATE_F16, 3_000_000, 5, 50, False, pf.RNG_PHILOX, True),  # 109 groups: k_top_wide over 2 tiles
+    (pf.STATE_F64, 1_100_000, 5, 50, False, pf.RNG_REFERENCE, True),  # fp64, 66 groups: k_top_wide
 ])
 def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy, rng, prune):
     """The two-launch path's streaming weighing pass (k_weigh_stream + k_group + k_top: resident blocks
     looping over the 256-particle blocks, the next particle's state prefetched) against the
     one-block-per-256-particles k_propagate_weigh: identical records, weights, propagated and resampled sets
     over a steady frame and an 80-iteration frame (one LED hidden), one tile of groups (140k) and several
-    (1.2M: 4,688 blocks in 74 groups), fp64 / fp32 / fp16 state, both RNG streams, pruned and unpruned."""
+    (1.2M: 4,688 blocks in 74 groups; 3M: 109 groups), fp64 / fp32 / fp16 state, both RNG streams, pruned and
+    unpruned.  Beyond one tile of groups the streaming pass's top is k_top_wide (16 waves, the per-tile passes
+    in parallel); the one-block pass keeps propagate_top's serial tiles."""
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 2)
     prior = st.prior(fast=True)
