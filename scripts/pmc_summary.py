@@ -15,7 +15,7 @@ import sys
 
 def short(name: str) -> str:
     for k in ("k_stage_multi", "k_propagate_weigh_multi", "k_resample_final_multi", "k_resample_multi",
-              "k_weigh_stream", "k_group", "k_top", "k_propagate_weigh", "k_resample_final", "k_resample", "k_frame2", "k_frame", "k_regen",
+              "k_weigh_stream", "k_group", "k_top_wide", "k_top", "k_propagate_weigh", "k_resample_final", "k_resample", "k_frame2", "k_frame", "k_regen",
               "k_import", "k_export", "k_weights_export"):
         if k in name:
             return k
