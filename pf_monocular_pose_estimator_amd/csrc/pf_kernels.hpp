@@ -1722,8 +1722,8 @@ __device__ __forceinline__ void publish_iteration(const FrameArgsT<T>& fa, T w, 
 // the block partials are plain stores read by k_group_top after the launch boundary (no arrival counters,
 // no group / top tail in this launch).  Per 256-particle block the arithmetic and the partial are exactly
 // k_propagate_weigh's, so the weights, partials and every later decision are bit-identical.
-// Occupancy floor of k_weigh_stream (waves per SIMD; 1 = the compiler's choice): the fp16 TUs set 6 (85 -> 80
-// VGPRs: C4 weighing 241 -> 233 us); 7 was slower at C4 and C5.
+// Occupancy floor of k_weigh_stream (waves per SIMD; 1 = the compiler's choice): the fp16 and fp32 TUs set 6
+// (85 -> 80 VGPRs: C4 weighing 241 -> 233 us, C5 30.6 -> 28.5 us); 7 was slower at C4 and C5.
 #ifndef PFMPE_WEIGH_STREAM_MIN_WAVES
 #define PFMPE_WEIGH_STREAM_MIN_WAVES 1
 #endif
