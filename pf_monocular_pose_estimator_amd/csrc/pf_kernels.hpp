@@ -2055,6 +2055,9 @@ __device__ __forceinline__ void propagate_weigh_block(
                             ctrl, gcount, tcount, nullptr, 0u, stamps, blk);
 }
 
+// Occupancy floor of k_propagate_weigh (waves per SIMD; 1 = the compiler's choice).  The fp32 / fp16 TUs set 6:
+// the 5- and 8-marker instances fit 8 waves anyway (63-66 VGPRs); the 12-marker one drops 93 -> 80 VGPRs
+// (5 -> 6 waves, a few values spilled): C3 weighing 96 -> 91 us.
 #ifndef PFMPE_WEIGH_MIN_WAVES
 #define PFMPE_WEIGH_MIN_WAVES 1
 #endif

@@ -5,6 +5,9 @@
 #ifndef PFMPE_WEIGH_STREAM_MIN_WAVES
 #define PFMPE_WEIGH_STREAM_MIN_WAVES 6  // k_weigh_stream: 6 waves per SIMD (85 -> 80 VGPRs)
 #endif
+#ifndef PFMPE_WEIGH_MIN_WAVES
+#define PFMPE_WEIGH_MIN_WAVES 6  // k_propagate_weigh: >= 6 waves per SIMD (12/16-marker instances)
+#endif
 #include "pfmpe_ctx.hpp"
 
 namespace pfmpe_impl {
