@@ -425,7 +425,7 @@ def main():
                  "accept_rate": sum(o.accepted for o in wo) / len(wo)}
 
     multi = None
-    sweep = args.multi_sweep or ("1,4,8,16" if world == 1 and config == "C2" and not args.occlude else "")
+    sweep = args.multi_sweep or ("1,4,8,16,32" if world == 1 and config == "C2" and not args.occlude else "")
     if sweep and rank == 0:  # untimed by the driver's contract: reported beside the line
         Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
         multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi), "
