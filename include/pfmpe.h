@@ -146,8 +146,14 @@ int pfmpe_step_batch(pfmpe_ctx* ctx, const pfmpe_frame_in* in, int n, pfmpe_fram
  * (plus iteration batches for streams whose exit rule does not fire at once).  in[s] / out[s] belong to
  * ctxs[s]; each context's outputs and state equal what pfmpe_step(ctxs[s], &in[s], &out[s]) gives.
  * All contexts must be distinct, on one device, of one state type, RNG mode and pruning option; the batch
- * runs on ctxs[0]'s HIP stream and uses ctxs[0]'s batch scratch.  Blocking.  Errors: PFMPE_E_ARG for a
- * mismatch (nothing launched), or the failing stream's error text in pfmpe_last_error(ctxs[0]). */
+ * runs on ctxs[0]'s HIP stream and uses ctxs[0]'s batch scratch.  Work a member context has pending on
+ * its own stream (an earlier pfmpe_step, ...) is ordered before the batch, and the member's next work on
+ * its own stream after it (events, only when the streams differ).  Blocking.  At most
+ * PFMPE_OPT_MULTI_MAX_BLOCKS (of ctxs[0]) 256-particle blocks per batch, in all: 160000 (~41M particles).
+ * Errors (nothing launched): PFMPE_E_ARG for a mismatch, the failing stream's own pfmpe_step code
+ * (E_ARG / E_CAP / E_STATE) for a bad frame, PFMPE_E_CAP above the block limit; the text, prefixed with
+ * the stream index, in pfmpe_last_error(ctxs[0]).  With PFMPE_OPT_TIMING set on ctxs[0] the batch's
+ * launches are timed into ctxs[0]'s kernel statistics (weighing, resampling, finishing, staging = aux). */
 int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pfmpe_frame_out* out);
 
 /* n consecutive batches of pfmpe_step_multi (in / out: n x S, batch-major), each blocking on its records
@@ -316,10 +322,13 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *                                  pfmpe_last_error describes it, the step still returns PFMPE_OK)
  *   PFMPE_OPT_FUSED_REARM   [0|n]  after such a fallback, switch one-launch frames back on after n clean
  *                                  two-launch frames (0: stay off)
+ *   PFMPE_OPT_MULTI_MAX_BLOCKS [160000|1..160000] largest pfmpe_step_multi batch this context leads, in
+ *                                  256-particle blocks (PFMPE_E_CAP above); the default is the tested limit
  * Within one process at most one one-launch frame runs per device at a time: a context that finds another
  * context's one-launch frame in flight on its device runs that frame as two launches (PFMPE_INFO_GUARD_SKIPS). */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4,
-       PFMPE_OPT_KEEP_PROPAGATED = 5, PFMPE_OPT_WAIT_BOUND_US = 6, PFMPE_OPT_FUSED_REARM = 7 };
+       PFMPE_OPT_KEEP_PROPAGATED = 5, PFMPE_OPT_WAIT_BOUND_US = 6, PFMPE_OPT_FUSED_REARM = 7,
+       PFMPE_OPT_MULTI_MAX_BLOCKS = 8 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* Context state for monitoring and tests (no reference counterpart: engine introspection). */

@@ -21,7 +21,7 @@ STATE_F32, STATE_F64, STATE_F16 = 0, 1, 2
 RNG_REFERENCE, RNG_PHILOX = 0, 1
 FLAG_ACCEPTED, FLAG_REINIT = 1, 4
 OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED = 1, 2, 3, 4, 5
-OPT_WAIT_BOUND_US, OPT_FUSED_REARM = 6, 7
+OPT_WAIT_BOUND_US, OPT_FUSED_REARM, OPT_MULTI_MAX_BLOCKS = 6, 7, 8
 OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
 DIAG_LAG_LOADS, DIAG_ABANDON, DIAG_NO_STREAM, DIAG_FORCE_STREAM, DIAG_SERIAL_TOP = 64, 128, 512, 1024, 2048
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2

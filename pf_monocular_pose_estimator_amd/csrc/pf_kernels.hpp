@@ -2150,14 +2150,31 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   }
 }
 
+// The block's stream and its stream-local block index, or -1 for a block the map does not place inside a
+// stream of this batch (never on a consistent batch: the host audits the layout before every launch,
+// pfmpe_ctx.hpp audit_batch; the guard keeps a corrupt map from turning into out-of-range accesses).
+template <typename T, typename SP>
+__device__ __forceinline__ int batch_block(const StreamDesc<T, SP>* __restrict__ descs,
+                                           const uint16_t* __restrict__ bmap, int S, int* s_out) {
+  const int s = __builtin_amdgcn_readfirstlane((int)bmap[blockIdx.x]);
+  if (s >= S) return -1;
+  const int blk = (int)blockIdx.x - __builtin_amdgcn_readfirstlane(descs[s].first_blk);
+  if (blk < 0 || blk >= __builtin_amdgcn_readfirstlane(descs[s].fa.nblk)) return -1;
+  *s_out = s;
+  return blk;
+}
+
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) void k_propagate_weigh_multi(const StreamDesc<T, SP>* __restrict__ descs,
-                                                                  const uint16_t* __restrict__ bmap, int iter) {
+                                                                  const uint16_t* __restrict__ bmap, int S, int iter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds sh;
-  const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
-  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP, true>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.table,
+  int s = 0;
+  const int blk = batch_block(descs, bmap, S, &s);
+  if (blk < 0) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  propagate_weigh_block<T, RNG, MAXM, PRUNE, SP, true>(d.fa, (const uint32_t*)&d.fa, blk, d.table,
                                                  d.prior, d.w0, d.w1, d.part0, d.part1, d.bscan0, d.bscan1, d.gpart0,
                                                  d.gpart1, d.gscan, d.ctrl, d.gcount_w, d.tcount_w, d.prop0, d.prop1,
                                                  iter, nullptr, smem, sc, sh);
@@ -2717,13 +2734,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RE
 
 template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_MIN_WAVES))) void k_resample_multi(
-    const StreamDesc<T, SP>* __restrict__ descs,
-                                                           const uint16_t* __restrict__ bmap) {
+    const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
-  const StreamDesc<T, SP>& d = descs[bmap[blockIdx.x]];
-  resample_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x - d.first_blk, d.ctrl, d.table,
+  int s = 0;
+  const int blk = batch_block(descs, bmap, S, &s);
+  if (blk < 0) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  resample_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, blk, d.ctrl, d.table,
                                    d.prior, d.post, d.w0, d.w1, d.bscan0, d.bscan1, d.gscan, d.cpart, d.cgroup,
                                    d.gcount_r, d.tcount_r, d.counts, d.cand, d.mlpose, d.out, d.seq, nullptr, d.prop0,
                                    d.prop1, sc, rec, sh);

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <string>
 #include <map>
+#include <memory>
 #include <vector>
 
 #include "../../include/pfmpe.h"
@@ -34,6 +35,15 @@ static_assert(PFMPE_MAX_BLOBS == kMaxBlobs, "blob capacity mismatch");
 struct EventPair {
   hipEvent_t a, b;
   int kid;
+};
+
+// An event recorded on a batch leader's stream after each batch it ran (pfmpe_step_multi).  Shared by the
+// batch's other contexts until their next work is ordered after it; destroyed with the last reference.
+struct BatchFence {
+  hipEvent_t ev = nullptr;
+  ~BatchFence() {
+    if (ev) (void)hipEventDestroy(ev);
+  }
 };
 
 struct pfmpe_ctx {
@@ -80,6 +90,7 @@ struct pfmpe_ctx {
   int64_t fused_rearm = 0;         // PFMPE_OPT_FUSED_REARM: clean two-launch frames before fusing again (0: never)
   int64_t clean_since_fallback = 0;
   int64_t wait_bound_us = 2000000; // PFMPE_OPT_WAIT_BOUND_US: bound of every in-launch wait
+  int64_t multi_max_blocks = 160000; // PFMPE_OPT_MULTI_MAX_BLOCKS: largest batch this context leads (blocks)
   int last_shape = -1;             // PFMPE_SHAPE_* of the last frame
   int last_weigh_pass = -1;        // PFMPE_WEIGH_* of the last two-launch weighing launch
   int64_t guard_skips = 0;         // one-launch frames run as two launches because another was in flight
@@ -105,6 +116,14 @@ struct pfmpe_ctx {
   unsigned char* h_multi = nullptr;
   unsigned char* hd_multi = nullptr;  // device address of h_multi
   size_t multi_cap = 0;
+  // Cross-stream ordering.  A context's work runs on its own stream (pfmpe_step, read-backs, ...) or, inside a
+  // batch, on the batch leader's stream.  last_stream is where its latest work went (nullptr: none since
+  // create); when the next work goes to a different stream it is ordered after that work: through the
+  // leader's fence when the latest work was a batch, else through own_ev recorded then on the own stream.
+  hipStream_t last_stream = nullptr;
+  std::shared_ptr<BatchFence> last_fence;
+  hipEvent_t own_ev = nullptr;
+  std::shared_ptr<BatchFence> lead_fence;  // this context as a batch leader
 
   // model / params
   int M = 0;
@@ -165,8 +184,30 @@ inline int fail(pfmpe_ctx* c, int code, const std::string& msg) {
       return fail((ctx), PFMPE_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
+// Order work about to be enqueued for context c on stream `to` after c's latest work, when that went to
+// another stream (a batch runs on the leader's stream, unordered with each member's own stream).
+// Free when consecutive work stays on one stream, which is every steady-state loop (pfmpe_step only, or
+// batches of the same contexts only).  err: the context that reports a failure.
+inline int order_after(pfmpe_ctx* c, hipStream_t to, pfmpe_ctx* err) {
+  if (!c->last_stream || c->last_stream == to) return PFMPE_OK;
+  if (c->last_fence) {
+    HIPCHK(err, hipStreamWaitEvent(to, c->last_fence->ev, 0));
+  } else {
+    if (!c->own_ev) HIPCHK(err, hipEventCreateWithFlags(&c->own_ev, hipEventDisableTiming));
+    HIPCHK(err, hipEventRecord(c->own_ev, c->last_stream));
+    HIPCHK(err, hipStreamWaitEvent(to, c->own_ev, 0));
+  }
+  c->last_stream = nullptr;
+  c->last_fence.reset();
+  return PFMPE_OK;
+}
+
+// Every C-ABI entry that enqueues work on the context's own stream starts here: the device, then the order
+// after the context's latest batch (if any).
 inline int set_device(pfmpe_ctx* c) {
   HIPCHK(c, hipSetDevice(c->device));
+  if (const int r_ = order_after(c, c->stream, c)) return r_;
+  c->last_stream = c->stream;
   return PFMPE_OK;
 }
 
@@ -294,6 +335,24 @@ inline int ensure_prop(pfmpe_ctx* c) {
   for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&c->d_prop[i], bytes));
   return PFMPE_OK;
 }
+
+// Batch scratch layout (pfmpe_step_multi), the same in the pinned host image and in HBM: host-supplied blob
+// tables [0, tbytes), then `na` stream descriptors from doff, then the uint16 block -> stream map of `total`
+// blocks from boff; `need` bytes in all.
+struct BatchLayout {
+  size_t doff, boff, need;
+};
+template <typename Desc>
+inline BatchLayout batch_layout(int na, int64_t total, size_t tbytes) {
+  BatchLayout L;
+  L.doff = tbytes;
+  L.boff = L.doff + ((size_t)na * sizeof(Desc) + 255) / 256 * 256;
+  L.need = L.boff + (size_t)total * sizeof(uint16_t) + 256;
+  return L;
+}
+// Blocks per batch accepted by pfmpe_step_multi (PFMPE_E_CAP above): the size the GPU tests cover
+// (tests/test_gpu_multi.py: 4 x 10M fp16 particles in one batch = 156,252 blocks; 32 x 1M in the bench).
+constexpr int64_t kMultiMaxBlocks = 160000;
 
 template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
@@ -507,21 +566,19 @@ struct Seq {
   // stream's blocks, one resampling launch, one finishing launch with a block per stream.  Streams whose exit
   // rule did not fire on the first iteration get further iteration batches (the others are not relaunched),
   // exactly as step()'s two-launch path does for one stream.  h / d: the batch scratch, whose first
-  // `tbytes` bytes already hold the host-supplied blob tables; tables[s] are device addresses.
+  // `tbytes` bytes already hold the host-supplied blob tables; tables[s] are device addresses.  The caller
+  // (multi_m) audited the layout of the whole batch (audit_batch); every later round is a subset of it.
   static int step_multi(pfmpe_ctx* const* cs, int S, const FrameArgsT<T>* fas, const unsigned char* const* tables,
                         unsigned char* h, const unsigned char* hdev, unsigned char* d, size_t tbytes) {
     using Desc = StreamDesc<T, SP>;
     pfmpe_ctx* c0 = cs[0];
-    hipStream_t st = c0->stream;
-    for (int s = 0; s < S; ++s) RET(ensure_prop(cs[s]));
     std::vector<int> act(S);
     for (int s = 0; s < S; ++s) act[s] = s;
-    const size_t doff = tbytes;
     int iter = 0, nb = 1;
     for (int round = 0;; ++round) {
       const int na = (int)act.size();
-      Desc* hd = (Desc*)(h + doff);
-      const size_t boff = doff + (((size_t)na * sizeof(Desc) + 255) / 256) * 256;
+      const BatchLayout L = batch_layout<Desc>(na, 0, tbytes);
+      Desc* hd = (Desc*)(h + L.doff);
       int64_t total = 0;
       size_t lds_w = 0, lds_f = 0;
       for (int i = 0; i < na; ++i) {
@@ -558,35 +615,49 @@ struct Seq {
         c->seq = (c->seq + 1) & 0x3fffffff;
         x.seq = c->seq;
         x.first_blk = (int32_t)total;
-          total += fa.nblk;
+        total += fa.nblk;
         lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.B));
         lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
       }
+      const BatchLayout Lt = batch_layout<Desc>(na, total, tbytes);
+      // iterations of this round: no launch past the largest remaining cap of the active streams (a launch past
+      // a stream's own cap would be a no-op on its ctrl->done, but it also runs with an iteration number the
+      // host's small-angle bound did not cover)
+      int room = 0;
+      for (int i = 0; i < na; ++i) {
+        const FrameArgsT<T>& fa = fas[act[i]];
+        room = std::max(room, (fa.force_iters > 0 ? fa.force_iters : std::max(1, fa.max_iter)) - iter);
+      }
+      const int nit = std::max(1, std::min(nb, room));
       // descriptors, host tables (first round) and the block map go to HBM by a staging launch in the same
       // stream (k_stage_multi reads the pinned image once), not by a copy-engine transfer
-      hipLaunchKernelGGL((k_stage_multi<T, SP>), dim3((unsigned)na), dim3(kBlock), 0, st, hdev, d,
-                         (uint32_t)doff, (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)boff);
-      HIPCHK(c0, hipGetLastError());
-      const Desc* dd = (const Desc*)(d + doff);
-      const uint16_t* db = (const uint16_t*)(d + boff);
-      for (int k = 0; k < nb; ++k, ++iter) {
-        if (c0->prune)
-          hipLaunchKernelGGL((k_propagate_weigh_multi<T, RNG, MAXM, true, SP>), dim3((unsigned)total), dim3(kBlock),
-                             lds_w, st, dd, db, iter);
-        else
-          hipLaunchKernelGGL((k_propagate_weigh_multi<T, RNG, MAXM, false, SP>), dim3((unsigned)total), dim3(kBlock),
-                             lds_w, st, dd, db, iter);
-        HIPCHK(c0, hipGetLastError());
+      const Desc* dd = (const Desc*)(d + Lt.doff);
+      const uint16_t* db = (const uint16_t*)(d + Lt.boff);
+      RET(launch_ext(c0, PFMPE_K_AUX, [&] {
+        klaunch(c0, k_stage_multi<T, SP>, dim3((unsigned)na), dim3(kBlock), 0, hdev, d, (uint32_t)Lt.doff,
+                (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)Lt.boff);
+      }));
+      for (int k = 0; k < nit; ++k, ++iter) {
+        RET(launch_ext(c0, PFMPE_K_PROPAGATE, [&] {
+          if (c0->prune)
+            klaunch(c0, k_propagate_weigh_multi<T, RNG, MAXM, true, SP>, dim3((unsigned)total), dim3(kBlock), lds_w, dd,
+                    db, na, iter);
+          else
+            klaunch(c0, k_propagate_weigh_multi<T, RNG, MAXM, false, SP>, dim3((unsigned)total), dim3(kBlock), lds_w,
+                    dd, db, na, iter);
+        }));
       }
-      hipLaunchKernelGGL((k_resample_multi<T, RNG, MAXM, SP>), dim3((unsigned)total), dim3(kBlock), 0, st, dd, db);
-      HIPCHK(c0, hipGetLastError());
-      hipLaunchKernelGGL((k_resample_final_multi<T, RNG, MAXM, SP>), dim3((unsigned)na), dim3(kFinalBlock), lds_f, st,
-                         dd);
-      HIPCHK(c0, hipGetLastError());
+      RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
+        klaunch(c0, k_resample_multi<T, RNG, MAXM, SP>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
+      }));
+      RET(launch_ext(c0, PFMPE_K_FINAL, [&] {
+        klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd);
+      }));
       std::vector<int> next;
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
-        if (wait_frame(c, st) != PFMPE_OK) return fail(c0, PFMPE_E_HIP, "step_multi: stream " + std::to_string(act[i]) + ": " + c->err);
+        if (wait_frame(c, c0->stream) != PFMPE_OK)
+          return fail(c0, PFMPE_E_HIP, "step_multi: stream " + std::to_string(act[i]) + ": " + c->err);
         if (!frame_done(c)) next.push_back(act[i]);
       }
       if (next.empty()) break;
@@ -598,6 +669,7 @@ struct Seq {
       act.swap(next);
       nb = round == 0 ? 1 : std::min(nb * 2, 16);
     }
+    if (c0->timing_now) HIPCHK(c0, hipStreamSynchronize(c0->stream));  // the brackets' end events completed
     for (int s = 0; s < S; ++s) {
       cs[s]->last_shape = PFMPE_SHAPE_TWO_LAUNCH;
       last_args<T>(cs[s]) = fas[s];
@@ -631,11 +703,56 @@ int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* tabl
   return Seq<T, RNG, 16, SP>::step(c, fa, table);
 }
 
+// Host-side bounds audit of a batch (the batched fault at 8 x 10M fp16 streams).  Everything a
+// batched kernel indexes is derived here from the descriptors it will read, and checked against what each
+// context allocated at create (pfmpe_create: max_blk blocks, max_grp = max_blk groups, ld-element planes,
+// a blob bank of bank_off.back() bytes) and against the batch scratch: a stream's blocks, groups, planes,
+// table, count partials and candidates all stay inside its own buffers, the block map covers [0, total)
+// exactly once, and the scratch holds tables + descriptors + map.  A failing check returns PFMPE_E_STATE
+// (a bug, never an input error: check_step validated the inputs) instead of launching.
+template <typename T, typename SP>
+int audit_batch(pfmpe_ctx* const* cs, int S, const FrameArgsT<T>* fas, const pfmpe_frame_in* in,
+                const std::vector<size_t>& toff, size_t tbytes, int64_t total, size_t cap) {
+  pfmpe_ctx* c0 = cs[0];
+  auto bad = [&](int s, const char* what) {
+    return fail(c0, PFMPE_E_STATE, "step_multi: batch audit failed for stream " + std::to_string(s) + ": " + what);
+  };
+  int64_t first = 0;
+  for (int s = 0; s < S; ++s) {
+    const pfmpe_ctx* c = cs[s];
+    const FrameArgsT<T>& fa = fas[s];
+    if (fa.N != c->N || fa.N < 1 || fa.N > c->max_particles || (int64_t)fa.N > c->ld) return bad(s, "particle count");
+    if (fa.nblk != (fa.N + kBlock - 1) / kBlock || fa.nblk > c->max_blk) return bad(s, "block count");
+    if (fa.gsz < 1 || fa.gsz > kGroup || fa.ngrp != (fa.nblk + fa.gsz - 1) / fa.gsz || fa.ngrp > c->max_grp)
+      return bad(s, "group count");
+    if (fa.ld != c->ld) return bad(s, "plane stride");
+    if (c->state_dtype != PFMPE_STATE_F64 && (int64_t)kPlanes * c->ld * (int64_t)c->es >= ((int64_t)1 << 32))
+      return bad(s, "plane buffer resource range");
+    if (fa.M != c->M || fa.M < 1 || fa.M > c->max_markers || fa.B < 0 || fa.B > c->max_blobs) return bad(s, "M / B");
+    if (c->keep_prop && (!c->d_prop[0] || !c->d_prop[1])) return bad(s, "kept propagated set not allocated");
+    if (c->record_counts && !c->d_counts) return bad(s, "count buffer not allocated");
+    if (in[s].bank_frame >= 0) {
+      const size_t f = (size_t)in[s].bank_frame;
+      if (!c->d_bank || f >= c->bank_B.size() || c->bank_B[f] != fa.B ||
+          c->bank_off[f] + BlobTable<T>::bytes(fa.B) > c->bank_off.back())
+        return bad(s, "bank table");
+    } else if (toff[s] + BlobTable<T>::bytes(fa.B) > tbytes) {
+      return bad(s, "host table");
+    }
+    first += fa.nblk;
+  }
+  if (first != total || total < 1 || total > kMultiMaxBlocks) return bad(0, "block total");
+  if (batch_layout<StreamDesc<T, SP>>(S, total, tbytes).need > cap) return bad(0, "batch scratch");
+  return PFMPE_OK;
+}
+
 // pfmpe_step_multi for S validated contexts of one (state type, RNG): frame arguments and blob tables
-// (host-supplied tables staged into the batch scratch of cs[0]), then Seq::step_multi on the marker bucket of
-// the largest M.
+// (host-supplied tables staged into the batch scratch of cs[0]), the bounds audit, the order after each
+// member's latest work on other streams, then Seq::step_multi on the marker bucket of the largest M, then the
+// fence every member's next work on its own stream is ordered after.
 template <typename T, int RNG, typename SP>
 int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
+  using Desc = StreamDesc<T, SP>;
   pfmpe_ctx* c0 = cs[0];
   std::vector<FrameArgsT<T>> fas(S);
   std::vector<size_t> toff(S, 0);
@@ -656,8 +773,14 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     total += fas[s].nblk;
     maxM = std::max(maxM, c->M);
   }
-  if (total > 65536 * 256) return fail(c0, PFMPE_E_CAP, "step_multi: too many blocks in one batch");
-  const size_t need = tbytes + ((size_t)S * sizeof(StreamDesc<T, SP>) + 255) / 256 * 256 + (size_t)total * 2 + 256;
+  const int64_t max_blocks = std::min(kMultiMaxBlocks, c0->multi_max_blocks);
+  if (total > max_blocks)
+    return fail(c0, PFMPE_E_CAP, "step_multi: " + std::to_string(total) + " blocks in one batch (at most " +
+                                     std::to_string(max_blocks) + " = " + std::to_string(max_blocks * kBlock) +
+                                     " particles, PFMPE_OPT_MULTI_MAX_BLOCKS)");
+  // every member's work so far is ordered before the batch (its own stream, or an earlier batch led elsewhere)
+  for (int s = 0; s < S; ++s) RET(order_after(cs[s], c0->stream, c0));
+  const size_t need = batch_layout<Desc>(S, total, tbytes).need;
   if (need > c0->multi_cap) {
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
     if (c0->d_multi) HIPCHK(c0, hipFree(c0->d_multi));
@@ -673,6 +796,8 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     HIPCHK(c0, hipHostGetDevicePointer((void**)&c0->hd_multi, c0->h_multi, 0));
     c0->multi_cap = cap;
   }
+  for (int s = 0; s < S; ++s) RET(ensure_prop(cs[s]));
+  RET((audit_batch<T, SP>(cs, S, fas.data(), in, toff, tbytes, total, c0->multi_cap)));
   std::vector<const unsigned char*> tables(S);
   for (int s = 0; s < S; ++s) {
     pfmpe_ctx* c = cs[s];
@@ -683,11 +808,28 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
       tables[s] = c0->d_multi + toff[s];
     }
   }
-  if (maxM <= 5) return Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
-  if (maxM <= 8) return Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
-  if (maxM <= 12)
-    return Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
-  return Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  int rc;
+  if (maxM <= 5)
+    rc = Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  else if (maxM <= 8)
+    rc = Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  else if (maxM <= 12)
+    rc = Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  else
+    rc = Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  // the batch's kernels may still be retiring when the records are in: each member's next work on its own
+  // stream waits for the fence (the leader's own stream is the batch stream)
+  if (!c0->lead_fence) {
+    auto f = std::make_shared<BatchFence>();
+    HIPCHK(c0, hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
+    c0->lead_fence = f;
+  }
+  HIPCHK(c0, hipEventRecord(c0->lead_fence->ev, c0->stream));
+  for (int s = 0; s < S; ++s) {
+    cs[s]->last_stream = c0->stream;
+    cs[s]->last_fence = s == 0 ? nullptr : c0->lead_fence;
+  }
+  return rc;
 }
 
 template <typename T, int RNG, typename SP>

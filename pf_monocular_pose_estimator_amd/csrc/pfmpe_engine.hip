@@ -256,6 +256,10 @@ void pfmpe_destroy(pfmpe_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->last_fence) (void)hipEventSynchronize(c->last_fence->ev);  // a batch led by another context
+  c->last_fence.reset();
+  c->lead_fence.reset();
+  if (c->own_ev) (void)hipEventDestroy(c->own_ev);
   free_all(c);
   delete c;
 }
@@ -316,6 +320,10 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       return PFMPE_OK;
     case PFMPE_OPT_KEEP_PROPAGATED:
       c->keep_prop = value != 0;
+      return PFMPE_OK;
+    case PFMPE_OPT_MULTI_MAX_BLOCKS:
+      if (value < 1 || value > kMultiMaxBlocks) return fail(c, PFMPE_E_ARG, "set_option: MULTI_MAX_BLOCKS is 1 .. 160000");
+      c->multi_max_blocks = value;
       return PFMPE_OK;
     case PFMPE_OPT_TIMING:
       if (value < 0 || value > (1 << 20)) return fail(c, PFMPE_E_ARG, "set_option: timing period out of range");
@@ -433,9 +441,11 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
       return fail(c0, PFMPE_E_ARG, who + "device, state type, RNG mode and pruning must match ctxs[0]");
     for (int e = 0; e < s; ++e)
       if (ctxs[e] == c) return fail(c0, PFMPE_E_ARG, who + "context appears twice");
-    if (check_step(c, &in[s], &out[s]) != PFMPE_OK) return fail(c0, PFMPE_E_ARG, who + c->err);
+    const int rc = check_step(c, &in[s], &out[s]);
+    if (rc != PFMPE_OK) return fail(c0, rc, who + c->err);  // the per-stream code (E_ARG / E_CAP / E_STATE)
   }
   RET(set_device(c0));
+  c0->timing_now = c0->timing > 0 && (c0->timing_frame++ % c0->timing) == 0;  // batches timed on the leader
   const bool ref = c0->params.rng_mode == PFMPE_RNG_REFERENCE;
   int rs;
   switch (c0->state_dtype) {
@@ -448,8 +458,16 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
     default:
       rs = ref ? multi_m<float, kRngReference, float>(ctxs, S, in) : multi_m<float, kRngPhilox, float>(ctxs, S, in);
   }
+  if (c0->timing_now) {
+    c0->timing_now = false;
+    if (rs == PFMPE_OK) RET(harvest_timing(c0));
+    c0->ev_used = 0;
+  }
   RET(rs);
-  for (int s = 0; s < S; ++s) take_step(ctxs[s], &in[s], &out[s]);
+  for (int s = 0; s < S; ++s) {
+    take_step(ctxs[s], &in[s], &out[s]);
+    if (!ctxs[s]->fused) ctxs[s]->clean_since_fallback += 1;  // a clean two-launch frame (PFMPE_OPT_FUSED_REARM)
+  }
   return PFMPE_OK;
 }
 

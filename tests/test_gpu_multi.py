@@ -173,3 +173,163 @@ def test_multi_rejects_mixed_contexts():
     finally:
         a.close()
         b.close()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# Large streams (a batch of 8 x 10M fp16 streams faulted once, and the batched tests stopped at
+# 100k particles / 7 groups per stream).  At 3M particles a stream has 11,719 blocks in 184 groups of 64 (the
+# in-launch tree hand-off walks 3 tiles of groups), at 10M 39,063 blocks in 611 groups (10 tiles).  Each
+# batched stream must equal its own pfmpe_step bit for bit: every record field, the kept weights and the
+# resampled set (compared as SHA-1 digests: 10M x 12 doubles per stream).
+
+def _big_streams(S, N, n_frames, seed0=0):
+    return [syn.make_stream(syn.StreamConfig("big", M=5, B=50, N=N, seed=seed0 + s), n_frames) for s in range(S)]
+
+
+def _big_engine(st, N, state=pf.STATE_F16):
+    e = pf.Engine(device=0, max_particles=N, state_dtype=state)
+    e.set_option(pf.OPT_FUSED, 0)
+    e.set_model(st.markers, st.K)
+    e.set_params(pf.default_params())
+    if getattr(st, "_prior", None) is None or len(st._prior) != N:  # one prior per stream (batch and solo engines)
+        st._prior = st.prior(N)
+    e.set_prior(st._prior)
+    e.stage_blob_bank([f.blobs for f in st.frames])
+    return e
+
+
+def _big_frame(e, st, f, s):
+    fr = st.frames[f]
+    return e.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, B=len(fr.blobs), bank_frame=f, dt=fr.dt,
+                        seed=(s << 32) + 17 + f, frame_idx=f)
+
+
+def _digest(a):
+    import hashlib
+    return hashlib.sha1(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def _big_compare(batch, solo, outs, streams, f):
+    for s, st in enumerate(streams):
+        ref = solo[s].step(_big_frame(solo[s], st, f, s))
+        a, b = outs[s].as_dict(), ref.as_dict()
+        for k in a:
+            if isinstance(a[k], np.ndarray):
+                assert np.array_equal(a[k], b[k]), (s, f, k)
+            else:
+                assert a[k] == b[k], (s, f, k, a[k], b[k])
+        assert _digest(batch[s].get_weights()) == _digest(solo[s].get_weights()), (s, f, "weights")
+        if a["resampled"]:
+            assert _digest(batch[s].get_particles(1)) == _digest(solo[s].get_particles(1)), (s, f, "resampled set")
+
+
+@pytest.mark.parametrize("S,N,frames", [(2, 3_000_000, 2), (2, 10_000_000, 2)])
+def test_multi_large_fp16_streams_bit_identical(S, N, frames):
+    streams = _big_streams(S, N, frames)
+    batch = [_big_engine(st, N) for st in streams]
+    solo = [_big_engine(st, N) for st in streams]
+    try:
+        for f in range(frames):
+            outs = pf.Engine.step_multi(batch, [_big_frame(batch[s], st, f, s) for s, st in enumerate(streams)])
+            assert all(o.accepted == 1 for o in outs)
+            _big_compare(batch, solo, outs, streams, f)
+    finally:
+        for e in batch + solo:
+            e.close()
+
+
+def test_multi_large_concurrent_batches():
+    """4 x 10M fp16 streams: one batch of all four (156,252 blocks, just below the batch limit), then the same
+    streams as two concurrent batches of two on two host threads (the configuration of the round-2 fault);
+    every stream equals its pfmpe_step run."""
+    import threading
+    S, N, frames = 4, 10_000_000, 2
+    streams = _big_streams(S, N, frames, seed0=10)
+    batch = [_big_engine(st, N) for st in streams]
+    solo = [_big_engine(st, N) for st in streams]
+    try:
+        outs = pf.Engine.step_multi(batch, [_big_frame(batch[s], st, 0, s) for s, st in enumerate(streams)])
+        _big_compare(batch, solo, outs, streams, 0)
+        res, errs = {}, []
+
+        def run(part):
+            try:
+                o = pf.Engine.step_multi([batch[s] for s in part], [_big_frame(batch[s], streams[s], 1, s) for s in part])
+                res.update(zip(part, o))
+            except Exception as ex:  # noqa: BLE001
+                errs.append(repr(ex))
+
+        th = [threading.Thread(target=run, args=(p,)) for p in ([0, 2], [1, 3])]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        _big_compare(batch, solo, [res[s] for s in range(S)], streams, 1)
+    finally:
+        for e in batch + solo:
+            e.close()
+
+
+def test_multi_block_limit():
+    """A batch above PFMPE_OPT_MULTI_MAX_BLOCKS is refused with PFMPE_E_CAP and nothing runs; the same
+    streams then batch normally under the default limit."""
+    st = syn.make_stream(syn.StreamConfig("m", M=5, B=50, N=100_000), 1)
+    fr = st.frames[0]
+    engs = [_engine(100_000, 5, pf.STATE_F32, pf.RNG_PHILOX) for _ in range(2)]
+    try:
+        for e in engs:
+            e.set_prior(st.prior())
+        ins = [e.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=fr.blobs, dt=fr.dt, seed=5 + s,
+                            frame_idx=0) for s, e in enumerate(engs)]
+        engs[0].set_option(pf.OPT_MULTI_MAX_BLOCKS, 500)  # 2 x 391 blocks
+        with pytest.raises(pf.PFError) as ei:
+            pf.Engine.step_multi(engs, ins)
+        assert ei.value.code == pf.E_CAP
+        with pytest.raises(pf.PFError):
+            engs[0].set_option(pf.OPT_MULTI_MAX_BLOCKS, 160_001)
+        engs[0].set_option(pf.OPT_MULTI_MAX_BLOCKS, 160_000)
+        outs = pf.Engine.step_multi(engs, ins)
+        assert all(o.accepted == 1 for o in outs)
+        bad = engs[1].make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=np.zeros((2000, 2)),
+                                 dt=fr.dt, seed=1, frame_idx=1)
+        with pytest.raises(pf.PFError) as ei:  # B above max_blobs: the stream's own pfmpe_step code
+            pf.Engine.step_multi(engs, [ins[0], bad])
+        assert ei.value.code == pf.E_CAP
+    finally:
+        for e in engs:
+            e.close()
+
+
+@pytest.mark.parametrize("state", [pf.STATE_F32, pf.STATE_F16])
+def test_multi_interleaved_with_single_steps(state):
+    """a batch runs on the leader's stream, each member's pfmpe_step / read-backs on its own.
+    Frames alternate per stream between the batch and pfmpe_step (and each frame's counts are read right
+    away), with the leader changing between frames; every stream must equal a stream stepped only with
+    pfmpe_step.  N = 300k: two-launch frames, so kernels are still retiring when records arrive."""
+    S, N, frames = 3, 300_000, 6
+    streams = _big_streams(S, N, frames, seed0=30)
+    mixed = [_big_engine(st, N, state) for st in streams]
+    solo = [_big_engine(st, N, state) for st in streams]
+    for e in mixed + solo:
+        e.set_option(pf.OPT_RECORD_COUNTS, 1)
+    try:
+        for f in range(frames):
+            batched = [s for s in range(S) if (s + f) % 3 != 0]  # two streams batched, one stepped alone
+            lead = batched[f % len(batched)]
+            order = [lead] + [s for s in batched if s != lead]
+            outs = dict(zip(order, pf.Engine.step_multi([mixed[s] for s in order],
+                                                        [_big_frame(mixed[s], streams[s], f, s) for s in order])))
+            for s in range(S):
+                if s not in outs:
+                    outs[s] = mixed[s].step(_big_frame(mixed[s], streams[s], f, s))
+                counts = mixed[s].get_counts()
+                ref = solo[s].step(_big_frame(solo[s], streams[s], f, s))
+                assert outs[s].as_dict()["winner_idx"] == ref.winner_idx, (s, f)
+                assert np.array_equal(counts, solo[s].get_counts()), (s, f)
+                assert np.array_equal(outs[s].as_dict()["winner_pose"], ref.as_dict()["winner_pose"]), (s, f)
+        for s in range(S):
+            assert _digest(mixed[s].get_particles(1)) == _digest(solo[s].get_particles(1)), s
+    finally:
+        for e in mixed + solo:
+            e.close()
