@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-frame trace of the closed-loop tracker pair (tests/test_gpu_closed_loop.py): both loops' winner,
+pairs, iterations and the refined pose's error against the synthetic truth.
+
+    python scripts/diag_closed_loop.py [--config C2] [--frames 20] [--state f32]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import pf_monocular_pose_estimator_amd as pf  # noqa: E402
+from pf_monocular_pose_estimator_amd import synthetic as syn  # noqa: E402
+from test_gpu_closed_loop import run_pair, rotation_angle  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--frames", type=int, default=20)
+    ap.add_argument("--state", default="f32", choices=["f32", "f64", "f16"])
+    a = ap.parse_args()
+    state = {"f32": pf.STATE_F32, "f64": pf.STATE_F64, "f16": pf.STATE_F16}[a.state]
+    rng = pf.RNG_REFERENCE if a.state == "f64" else pf.RNG_PHILOX
+    cfg = syn.CONFIGS[a.config]
+    st = syn.make_stream(cfg, a.frames)
+    rows = run_pair(cfg, a.frames, state, rng)
+    for f, (out, ref, pe, po) in enumerate(rows):
+        T = st.frames[f].truth
+        et = lambda p: np.abs(p[[3, 7, 11]] - T[:3, 3]).max()  # noqa: E731
+        er = lambda p: rotation_angle(syn.to44(p)[:3, :3], T[:3, :3])  # noqa: E731
+        print(f"frame {f}: eng it {out['iters']} win {out['winner_idx']} hp {out['highest_prob']:.4f} "
+              f"pairs {out['pairs'].tolist()} | orc it {ref['iters']} win {ref['winner_idx']} hp {ref['highest_prob']:.4f} "
+              f"pairs {ref['pairs'].tolist()}")
+        print(f"   eng err {et(pe):.2e} m {er(pe):.2e} rad | orc err {et(po):.2e} m {er(po):.2e} rad | "
+              f"diff {np.abs(pe[[3, 7, 11]] - po[[3, 7, 11]]).max():.2e} m")
+
+
+if __name__ == "__main__":
+    main()

@@ -82,7 +82,8 @@ CASES = [  # (N, M, B, heavy)
 @pytest.mark.parametrize("fused", [2, 1, 0])  # flat one launch / tree one launch / two launches
 def test_fp64_exact_trajectory(rng, N, M, B, heavy, prune, fused):
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
-    st = syn.make_stream(cfg, 3)
+    n_frames = 10
+    st = syn.make_stream(cfg, n_frames)
     prm = pf.default_params()
     prm.rng_mode = RNG[rng]
     eng = make_engine(N, st.markers, st.K, pf.STATE_F64, RNG[rng], prune=prune, fused=fused)
@@ -245,7 +246,8 @@ def test_fp32_tolerance(rng, N, M, B, heavy):
     against the oracle's resampler run on the GPU's OWN weights (exact), and outputs are checked by the
     north_star criterion: refined (Gauss-Newton) poses within 1e-4 m / 1e-3 rad."""
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
-    st = syn.make_stream(cfg, 3)
+    n_frames = 10
+    st = syn.make_stream(cfg, n_frames)
     prm = pf.default_params()
     prm.rng_mode = RNG[rng]
     eng = make_engine(N, st.markers, st.K, pf.STATE_F32, RNG[rng])
@@ -279,7 +281,7 @@ def test_fp32_tolerance(rng, N, M, B, heavy):
                 assert rotation_angle(syn.to44(pg)[:3, :3], syn.to44(pr)[:3, :3]) < 1e-3
                 compared += 1
     # the pose criterion must actually have been applied (not vacuously skipped on differing winners)
-    assert compared >= 2, compared
+    assert compared >= n_frames - 1, compared
     eng.close()
 
 
