@@ -71,7 +71,8 @@ def parse():
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
     ap.add_argument("--multi-sweep", default="",
                     help="after the timed region, also run S independent streams of the config per GPU as one "
-                         "batch (pfmpe_step_multi) for each S in this comma list; default 1,4,8,16 at C2 on one GPU")
+                         "batch (pfmpe_step_multi) for each S in this comma list; default 1,4,8,16,32 at C2 on one "
+                         "GPU; 'none' skips the sweep")
     ap.add_argument("--multi-steps", type=int, default=50, help="timed batches per multi-stream point")
     ap.add_argument("--multi-groups", default="1,2",
                     help="batches per multi-stream point, each on its own host thread and HIP stream (comma list)")
@@ -426,6 +427,8 @@ def main():
 
     multi = None
     sweep = args.multi_sweep or ("1,4,8,16,32" if world == 1 and config == "C2" and not args.occlude else "")
+    if sweep == "none":
+        sweep = ""
     if sweep and rank == 0:  # untimed by the driver's contract: reported beside the line
         Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
         multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi), "

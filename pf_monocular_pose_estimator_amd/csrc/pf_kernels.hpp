@@ -445,16 +445,32 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const Lds
 // README.md:95-143; the host checks, FrameArgsT::k_upper): the zero terms are skipped, 16 instead of 36
 // operations.  A skipped term is an exact +-0 added before the first rounding, so the sums are the same
 // except for the sign of an exact zero.  fp64 (the parity mode) keeps the literal form.
+// fp32 pairs for the packed VALU forms (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: two fp32 operations per
+// instruction).  Each lane of a pair sees exactly the scalar operation sequence (mul, fma, add rounded the
+// same way; the TUs are built with -ffp-contract=off, so nothing else fuses), so packed and scalar forms
+// give the same bits.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 pk2(float a, float b) { return f32x2{a, b}; }
+
 template <typename T>
 __device__ __forceinline__ void k_times_pose(const LdsConst<T>& sc, const T* P, bool k_upper, T* Q) {
   if (std::is_same<T, float>::value && k_upper) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      T s = sc.K[0] * P[0 * 4 + j];
-      s = fmadd(sc.K[1], P[1 * 4 + j], s);
-      Q[0 * 4 + j] = fmadd(sc.K[2], P[2 * 4 + j], s);
-      Q[1 * 4 + j] = fmadd(sc.K[5], P[2 * 4 + j], sc.K[4] * P[1 * 4 + j]);
+    for (int j = 0; j < 4; j += 2) {  // columns j, j + 1 as one pair
+      const f32x2 p0 = pk2(P[0 * 4 + j], P[0 * 4 + j + 1]);
+      const f32x2 p1 = pk2(P[1 * 4 + j], P[1 * 4 + j + 1]);
+      const f32x2 p2 = pk2(P[2 * 4 + j], P[2 * 4 + j + 1]);
+      f32x2 s = p0 * sc.K[0];
+      s = pk_fma(pk2(sc.K[1], sc.K[1]), p1, s);
+      s = pk_fma(pk2(sc.K[2], sc.K[2]), p2, s);
+      const f32x2 s1 = pk_fma(pk2(sc.K[5], sc.K[5]), p2, p1 * sc.K[4]);
+      Q[0 * 4 + j] = s.x;
+      Q[0 * 4 + j + 1] = s.y;
+      Q[1 * 4 + j] = s1.x;
+      Q[1 * 4 + j + 1] = s1.y;
       Q[2 * 4 + j] = P[2 * 4 + j];
+      Q[2 * 4 + j + 1] = P[2 * 4 + j + 1];
     }
     return;
   }
@@ -476,6 +492,27 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
                                                 T* v) {
   T Q[12];
   k_times_pose<T>(sc, P, fa.k_upper != 0, Q);
+  if constexpr (std::is_same<T, float>::value) {  // rows 0 and 1 as one packed pair, same operations
+    // every slot up to MAXM is projected (markers past M are zeros, their u / v never read): no branch, so the
+    // u / v arrays stay in registers (a conditional store per slot had put them in scratch)
+    const f32x2 q0 = pk2(Q[0], Q[4]), q1 = pk2(Q[1], Q[5]), q2 = pk2(Q[2], Q[6]), q3 = pk2(Q[3], Q[7]);
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      const float X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
+      f32x2 s = q0 * X;
+      s = pk_fma(q1, pk2(Y, Y), s);
+      s = pk_fma(q2, pk2(Z, Z), s);
+      s = s + q3;
+      float z = Q[8] * X;
+      z = fmadd(Q[9], Y, z);
+      z = fmadd(Q[10], Z, z);
+      z = z + Q[11];
+      const f32x2 uv = s * rcp_t(z);  // persp(): p0 * rcp(p2), p1 * rcp(p2)
+      u[j] = uv.x;
+      v[j] = uv.y;
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     if (j < fa.M) {
@@ -587,10 +624,10 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
         }
         visited += c1 - c0;
         const float uj = u[j], vj = v[j];
+        const f32x2 uvj = pk2(uj, vj);
         auto visit = [&](BlobXY<float> p, int o, bool in) {
-          const float dx = p.x - uj;
-          const float dy = p.y - vj;
-          const float d = fmadd(dx, dx, dy * dy);
+          const f32x2 dd = pk2(p.x, p.y) - uvj;  // (dx, dy) in one v_pk_add_f32
+          const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
           const uint64_t key = ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)o;
           best = (in & (key < best)) ? key : best;
         };

@@ -80,7 +80,27 @@ struct U32x4 {
   uint32_t x, y, z, w;
 };
 
+// a ^ b ^ k in ONE instruction on the device: gfx950's three-input bitwise op (truth table 0x96 = xor3), the
+// round key k an SGPR operand
+PF_HD uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+  return r;
+#else
+  return a ^ b ^ k;
+#endif
+}
+
+// The key must be wave-uniform (every call site passes the frame's seed).  On the device the round keys are
+// derived from the key right here by scalar adds: the empty asm keeps the compiler from hoisting all twenty
+// of them out of the streaming loops, where they held 20 SGPRs, spilled to VGPR lanes and cost a
+// v_readlane + s_nop per use; the two per-round xors are one v_bitop3 (10 rounds: 20 v_mad_u64_u32 +
+// 20 v_bitop3 per call, round keys on the scalar unit).
 PF_HD U32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(k0), "+s"(k1));
+#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     if (r) {
@@ -89,9 +109,9 @@ PF_HD U32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, ui
     }
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n0 = xor3_key((uint32_t)(p1 >> 32), c1, k0);
     const uint32_t n1 = (uint32_t)p1;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n2 = xor3_key((uint32_t)(p0 >> 32), c3, k1);
     const uint32_t n3 = (uint32_t)p0;
     c0 = n0; c1 = n1; c2 = n2; c3 = n3;
   }
