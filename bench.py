@@ -76,6 +76,8 @@ def parse():
     ap.add_argument("--multi-steps", type=int, default=50, help="timed batches per multi-stream point")
     ap.add_argument("--multi-groups", default="1,2",
                     help="batches per multi-stream point, each on its own host thread and HIP stream (comma list)")
+    ap.add_argument("--exact-steps", type=int, default=100,
+                    help="frames of the fp64 / reference-RNG (parity mode) C2 point beside the default line (0 = skip)")
     ap.add_argument("--scale-ref-steps", type=int, default=100,
                     help="frames of the one-GPU C5 reference beside the default C2 line (0 = skip)")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
@@ -306,12 +308,14 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
             e.close()
 
 
-def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args):
-    """One stream of `base` (f32 state) on one GPU, timed as the main line is (pfmpe_step_batch: every frame
-    blocks on its record)."""
+def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args,
+                        state_dtype=None):
+    """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
+    every frame blocks on its record)."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
     st = syn.make_stream(cfg, warmup + steps)
-    eng = pf.Engine(device=device, max_particles=cfg.N, state_dtype=pf.STATE_F32)
+    eng = pf.Engine(device=device, max_particles=cfg.N,
+                    state_dtype=pf.STATE_F32 if state_dtype is None else state_dtype)
     try:
         eng.set_model(st.markers, st.K)
         prm = pf.default_params()
@@ -426,23 +430,40 @@ def main():
                  "accept_rate": sum(o.accepted for o in wo) / len(wo)}
 
     multi = None
+    default_line = world == 1 and config == "C2" and not args.config and not args.occlude
     sweep = args.multi_sweep or ("1,4,8,16,32" if world == 1 and config == "C2" and not args.occlude else "")
     if sweep == "none":
         sweep = ""
     if sweep and rank == 0:  # untimed by the driver's contract: reported beside the line
         Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
-        multi = {"what": "S independent streams of this config per GPU, one batch per frame (pfmpe_step_multi), "
+        multi = {"what": "S independent streams of a config per GPU, one batch per frame (pfmpe_step_multi), "
                          "split into `groups` concurrent batches (one host thread and HIP stream each); "
                          "frac = updates/s x (3S+8) B / 8 TB/s", "points": []}
         gsweep = [int(x) for x in args.multi_groups.split(",") if x]
-        for S_ in [int(x) for x in sweep.split(",") if x]:
-            for G_ in gsweep:
-                if G_ > 1 and S_ < 2 * G_:
-                    continue
-                pt = multi_stream_point(pf, syn, base, S_, args.multi_steps, 5, state_dtype, prm.rng_mode, device,
-                                        sid, args.prune, args.keep_prop, G_)
-                pt["frac"] = round(pt["updates_per_s"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
-                multi["points"].append(pt)
+        plan = [(base, state_dtype, Sb, S_, G_) for S_ in [int(x) for x in sweep.split(",") if x] for G_ in gsweep
+                if not (G_ > 1 and S_ < 2 * G_)]
+        if default_line and args.multi_sweep == "":
+            # HBM-sized batches: C5 streams (1M particles each; 8M / 32M live particles, above the
+            # 256 MiB MALL) as two concurrent batches, and two C4 streams (10M fp16 each) as one batch
+            plan += [(syn.CONFIGS["C5"], pf.STATE_F32, 48, 8, 2), (syn.CONFIGS["C5"], pf.STATE_F32, 48, 32, 2),
+                     (syn.CONFIGS["C4"], pf.STATE_F16, 24, 2, 1)]
+        for cfg_, st_, Sb_, S_, G_ in plan:
+            steps_ = args.multi_steps if cfg_.N <= 1_000_000 else max(10, args.multi_steps // 3)
+            pt = multi_stream_point(pf, syn, cfg_, S_, steps_, 5, st_, prm.rng_mode, device, sid, args.prune,
+                                    args.keep_prop, G_)
+            pt["config"] = cfg_.name
+            pt["state"] = {pf.STATE_F32: "f32", pf.STATE_F16: "f16", pf.STATE_F64: "f64"}[st_]
+            pt["frac"] = round(pt["updates_per_s"] * (3 * Sb_ + 8) / 1e9 / HBM_PEAK_GBPS, 4)
+            multi["points"].append(pt)
+
+    exact = None
+    if default_line and args.exact_steps > 0 and rank == 0:
+        # the parity mode's throughput (fp64 state, the reference's minstd stream: every count, index and pair
+        # equals the CPU oracle's), one C2 stream timed like the main line (untimed by the driver's contract)
+        exact = single_stream_point(pf, syn, base, args.exact_steps, 10, pf.RNG_REFERENCE, device, sid, args,
+                                    state_dtype=pf.STATE_F64)
+        exact["what"] = ("C2 in the parity mode: fp64 state + the reference's minstd_rand0 stream (counts, indices and "
+                         "pairs identical to the CPU oracle), timed like the main line")
 
     scale_ref = None
     if world == 1 and config == "C2" and not args.config and not args.occlude and args.scale_ref_steps > 0:
@@ -518,6 +539,7 @@ def main():
             "worst_case": worst,
             "multi_stream": multi,
             "scaling_reference": scale_ref,
+            "parity_mode": exact,
         }
         print(json.dumps(line), flush=True)
     eng.close()

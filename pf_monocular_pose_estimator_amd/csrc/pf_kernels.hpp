@@ -35,7 +35,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cmath>
+#include <cstring>
 #include <type_traits>
+#include <vector>
 
 #include <hip/hip_fp16.h>
 
@@ -60,6 +64,16 @@ enum : int { kRngReference = 0, kRngPhilox = 1 };
 
 // ----------------------------------------------------------------------------- kernel arguments
 // Passed by value (kernarg segment -> scalar loads), pre-converted to the compute type T on the host.
+// The frame's 2D blob grid as kernel arguments (scalar registers, reloadable from the kernarg segment /
+// stream descriptor instead of held in VGPRs): build_blob_table_host's GridHdr plus the byte offsets of the
+// grid's parts in the table; on = 0 when the table has no grid or one built for a narrower window.
+struct GridArgs {
+  float inv_c, gx0, gy0, pad0;     // cell of (u, v): ((u - gx0) * inv_c, (v - gy0) * inv_c), clamped (square cells)
+  float fmaxx, fmaxy;              // ncx - 1, ncy - 1
+  int32_t ncx, on;
+  int32_t cell_off, gxy_off, gorig_off, pad;  // table offsets: uint32 cell[], BlobXY<float> gxy[], int32 gorig[]
+};
+
 template <typename T>
 struct FrameArgsT {
   T cur[12], pred[12], predm[12], cam[12];  // 3x4 row-major
@@ -82,6 +96,9 @@ struct FrameArgsT {
   int32_t k_upper;                // K = [k0 k1 k2; 0 k4 k5; 0 0 1] (host check; fp32 skips the zero terms)
   uint32_t wait_ticks;            // bound of every in-launch wait, s_memrealtime ticks (100 MHz)
   uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
+  int32_t tbytes;                 // this frame's blob table, bytes (base + grid: build_blob_table_host)
+  int32_t pad_fa;
+  GridArgs grid;                  // the table's 2D grid (fp32 pruned column minima)
   int64_t ld;                     // SoA plane stride in elements
   T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
 };
@@ -449,6 +466,10 @@ __device__ __forceinline__ void make_particle(const FrameArgsT<T>& fa, const Lds
 // instruction).  Each lane of a pair sees exactly the scalar operation sequence (mul, fma, add rounded the
 // same way; the TUs are built with -ffp-contract=off, so nothing else fuses), so packed and scalar forms
 // give the same bits.
+// a * b + c for 0 <= a, b < 2^24: one full-rate v_mad_u32_u24 (v_mul_lo_u32 is quarter rate)
+__device__ __forceinline__ int mad24(int a, int b, int c) {
+  return (int)(((unsigned)a & 0xffffffu) * ((unsigned)b & 0xffffffu)) + c;
+}
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ f32x2 pk2(float a, float b) { return f32x2{a, b}; }
@@ -609,6 +630,55 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
     // in-range bucket: a NaN projection never takes a candidate).  The two roundings of xmin -+ tolq and
     // u - base are each within half an ulp of a pixel coordinate, like bucket_of's own, far inside tolq's
     // slack (1e-3 px + 0.1 %): the window still holds every blob within tol_PF.
+    // The 2D grid (when the table has one built for at least this frame's window): the candidates of marker j
+    // are the one cell list its projection falls in (build_blob_table_host proves every blob within tol_PF is
+    // listed there); ~1 candidate per marker instead of an x-strip's ~2, so the wave's candidate walk is
+    // usually a single step.  Otherwise the x-buckets.
+    const GridArgs& ga = fa.grid;
+    if (PRUNE && ga.on) {  // wave-uniform (host: the table's grid covers this frame's window)
+      // Grid walk: one cell list per marker (~1 candidate).  Its entries are in increasing original index, so
+      // a strict "closer" test keeps the first (lowest-index) of equally close blobs, the key order above,
+      // and a NaN distance is never taken.  The first two entries are visited unconditionally (masked by the
+      // list length; a read past a short list stays inside the table), so the common path has no loop.
+      const uint32_t* cell = (const uint32_t*)(tb.base + ga.cell_off);
+      const BlobXY<float>* cxy = (const BlobXY<float>*)(tb.base + ga.gxy_off);
+      const int32_t* corig = (const int32_t*)(tb.base + ga.gorig_off);
+#pragma unroll
+      for (int j = 0; j < MAXM; ++j) {
+        float bd = INFINITY;
+        int bo = 0;
+        if (j < M) {
+          const int cx = (int)__builtin_amdgcn_fmed3f((u[j] - ga.gx0) * ga.inv_c, 0.0f, ga.fmaxx);
+          const int cy = (int)__builtin_amdgcn_fmed3f((v[j] - ga.gy0) * ga.inv_c, 0.0f, ga.fmaxy);
+          const uint32_t rec = cell[mad24(cy, ga.ncx, cx)];
+          const int c0 = (int)(rec & 0xffffu), n = (int)(rec >> 16);
+          visited += n;
+          const f32x2 uvj = pk2(u[j], v[j]);
+          auto visit = [&](BlobXY<float> p, int o, bool in) {
+            const f32x2 dd = pk2(p.x, p.y) - uvj;  // (dx, dy) in one v_pk_add_f32
+            const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
+            const bool take = in & (d < bd);
+            bd = take ? d : bd;
+            bo = take ? o : bo;
+          };
+          {
+            const BlobXY<float> pa = cxy[c0], pb = cxy[c0 + 1];
+            const int oa = corig[c0], ob = corig[c0 + 1];
+            visit(pa, oa, n > 0);
+            visit(pb, ob, n > 1);
+          }
+          for (int c = c0 + 2; c < c0 + n; c += 2) {  // rare: a cell with more than two blobs
+            const BlobXY<float> pa = cxy[c], pb = cxy[c + 1];
+            const int oa = corig[c], ob = corig[c + 1];
+            visit(pa, oa, true);
+            visit(pb, ob, c + 1 < c0 + n);
+          }
+        }
+        m[j] = bd;
+        r[j] = bo;  // 0 unless a candidate was taken (a finite distance), as the key form's r
+      }
+      return visited;
+    }
     const float fmaxb = (float)(tb.nb - 1);
     const float base_lo = tb.xmin + fa.tolq, base_hi = tb.xmin - fa.tolq;
 #pragma unroll
@@ -779,7 +849,7 @@ __device__ __forceinline__ float score_unordered(const FrameArgsT<float>& fa, co
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
     const float d = sqrt_t(m[j]);
-    acc[j] = j < M && d <= tol_pf;
+    acc[j] = d <= tol_pf;  // markers past M have m = +inf (column_minima), never accepted
     const float q = (tol - d) * rtol;
     Pr = acc[j] ? Pr + (Mt + q * q) : Pr;
     bool dup = false;
@@ -1220,26 +1290,48 @@ __device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target, 
 
 
 // ============================================================================== kernels
-// ---- blob table (DESIGN.md "Exact blob pruning"): the frame's blobs grouped into bucket_count(B) x-buckets,
-// built once per frame on the host (build_blob_table_host, O(B)) and copied whole into each block's
-// LDS by the weighing pass.  Layout, every part 16-byte aligned:
-//   hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[nb+1] | BlobXY<T> xy[B] | int32 orig[B]
-// with nb = bucket_count(B).
-// Within a bucket blobs keep increasing original index.
+// ---- blob table (DESIGN.md "Exact blob pruning"), built once per frame on the host (build_blob_table_host,
+// O(B)) and copied whole into each block's LDS by the weighing kernels.  Layout, every part 16-byte aligned:
+//   base  hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[nb+1] | BlobXY<T> xy[B] | int32 orig[B]
+//         (the blobs grouped into nb = bucket_count(B) x-buckets, increasing original index within a bucket;
+//         every blob once: the linear scans of pose_pairs / k_resample_final and the fp64 pruned minima)
+//   grid  GridHdr | uint32 cell[ncell] (start | count << 16) | BlobXY<float> gxy[nent + 1] | int32 gorig[nent + 1]
+//         (fp32 tables: a 2D cell grid over the blobs' bounding box widened by the pruning half-window; cell c
+//         lists every blob whose +-tolq box (plus 0.01 px) overlaps it, so a marker's candidates are ONE
+//         cell's list.  ncell = 0: no grid, the x-buckets serve; fp64 tables and large B never build one)
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
+struct GridHdr {
+  float inv_c, gx0, gy0, pad0;     // cell of (u, v): ((u - gx0) * inv_c, (v - gy0) * inv_c), clamped
+  float fmaxx, fmaxy;              // ncx - 1, ncy - 1
+  float gtolq;                     // half-window the lists were built for (>= the frame's tolq to be used)
+  int32_t ncx, ncell, nent;        // columns, cells, list entries
+  int32_t pad[2];
+};
+static_assert(sizeof(GridHdr) == 48, "grid header");
+constexpr int kGridMaxCells = 1024;   // cell records: 4 KB
+constexpr int kGridMaxEntries = 1024; // list entries: 12 KB (B up to ~400 blobs at 2-3 cells each)
 template <typename T>
 struct BlobTable {
   static constexpr size_t off_bstart() { return align16(4 * sizeof(T)); }
   static constexpr size_t off_xy(int B) { return off_bstart() + align16((size_t)(bucket_count(B) + 1) * 4); }
   static constexpr size_t off_orig(int B) { return off_xy(B) + align16((size_t)B * sizeof(BlobXY<T>)); }
+  // the base part (every blob once): all the linear scans need
   static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
+  static constexpr size_t off_grid(int B) { return bytes(B); }
+  static constexpr size_t grid_bytes(int ncell, int nent) {
+    return sizeof(GridHdr) + align16((size_t)ncell * 4) + align16((size_t)(nent + 1) * 8) + align16((size_t)(nent + 1) * 4);
+  }
+  // a table's total size: base + grid (the host builder returns it; FrameArgsT::tbytes carries it)
+  static constexpr size_t total_bytes(int B, int ncell, int nent) { return bytes(B) + grid_bytes(ncell, nent); }
+  static constexpr size_t max_bytes() { return total_bytes(kMaxBlobs, kGridMaxCells, kGridMaxEntries); }
   // LDS of the weighing kernels: the table plus one 16-B granule, so the masked second candidate of the
-  // fp32 column_minima step (index c1 <= B) reads inside the allocation
-  static constexpr size_t lds_bytes(int B) { return bytes(B) + 16; }
+  // fp32 column_minima step reads inside the allocation
+  static constexpr size_t lds_bytes(size_t tbytes) { return tbytes + 16; }
 };
 
 template <typename T>
 struct LdsBlobs {
+  const unsigned char* base;  // the table (the grid's parts sit at FrameArgsT::grid offsets from it)
   const BlobXY<T>* bxy;
   const int32_t* orig;
   const int32_t* bstart;  // nb + 1
@@ -1251,6 +1343,7 @@ template <typename T>
 __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* base, int B) {
   LdsBlobs<T> t;
   const T* hdr = (const T*)base;
+  t.base = base;
   t.xmin = hdr[0];
   t.inv_bw = hdr[1];
   t.b0x = hdr[2];
@@ -1262,10 +1355,30 @@ __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* 
   return t;
 }
 
-// Host builder.  The bucket formula is bucket_of in T arithmetic (this TU: -ffp-contract=off), the
-// same expression the kernels evaluate for their query windows.
+// The kernel arguments of a table's grid (host): on only when the table has a grid built for at least the
+// frame's window (tolq: FrameArgsT::tolq of the frame).  gh: the table's GridHdr (at off_grid(B)).
 template <typename T>
-inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst) {
+inline GridArgs grid_args(const GridHdr& gh, int B, float tolq) {
+  GridArgs g{};
+  g.on = (gh.ncell > 0 && gh.gtolq >= tolq) ? 1 : 0;
+  if (!g.on) return g;
+  g.inv_c = gh.inv_c;
+  g.gx0 = gh.gx0;
+  g.gy0 = gh.gy0;
+  g.fmaxx = gh.fmaxx;
+  g.fmaxy = gh.fmaxy;
+  g.ncx = gh.ncx;
+  g.cell_off = (int32_t)(BlobTable<T>::off_grid(B) + sizeof(GridHdr));
+  g.gxy_off = g.cell_off + (int32_t)align16((size_t)gh.ncell * 4);
+  g.gorig_off = g.gxy_off + (int32_t)align16((size_t)(gh.nent + 1) * 8);
+  return g;
+}
+
+// Host builder; returns the table's size in bytes.  The bucket formula is bucket_of in T arithmetic (this TU:
+// -ffp-contract=off), the same expression the kernels evaluate for their query windows.  tolq: the pruning
+// half-window of the frames that will use the table (FrameArgsT::tolq, from tol_PF).
+template <typename T>
+inline size_t build_blob_table_host(const double* blobs, int B, double tolq, unsigned char* dst) {
   T xmin = (T)INFINITY, xmax = -(T)INFINITY;
   for (int i = 0; i < B; ++i) {
     const T x = (T)blobs[2 * i];
@@ -1298,6 +1411,92 @@ inline void build_blob_table_host(const double* blobs, int B, unsigned char* dst
     xy[pos].y = (T)blobs[2 * i + 1];
     orig[pos] = i;
   }
+  // ---- the grid (fp32 tables).  Device query: cell coordinate f = fl(fl(u - gx0) * inv_c), clamped by med3 to
+  // [0, ncx - 1], truncated.  Every blob within tol_PF of a query must be in the query's cell list:
+  //  * a blob is listed in every cell whose real-arithmetic interval [g(bx - m), g(bx + m)] it overlaps,
+  //    g(x) = (x - gx0) * inv_c with the fp32 constants the device uses, m = tolq + 0.01 px;
+  //  * the device's f differs from g(u) by two roundings (coordinates < 2^11 px: a few 1e-4 px), far below
+  //    the m - tol_PF >= 0.01 px slack; a clamped query (outside the widened box) has no blob within tolq at
+  //    all, so whatever its cell lists, its minimum fails the gate;
+  //  * every blob's own interval is clamped to the grid the same way.
+  // Each list holds its blobs in increasing original index (the fill below runs over i), so the device's
+  // strict "closer" comparison keeps the lowest index among equally close blobs: the reference's tie rule.
+  GridHdr* gh = (GridHdr*)(dst + BlobTable<T>::off_grid(B));
+  std::memset(gh, 0, sizeof(GridHdr));
+  size_t total = BlobTable<T>::total_bytes(B, 0, 0);
+  if (!std::is_same<T, float>::value || B == 0) return total;
+  const double m = tolq + 0.01;
+  double bx0 = INFINITY, bx1 = -INFINITY, by0 = INFINITY, by1 = -INFINITY;
+  for (int i = 0; i < B; ++i) {
+    const double x = (double)(float)blobs[2 * i], y = (double)(float)blobs[2 * i + 1];
+    if (!(x - x == 0.0) || !(y - y == 0.0)) return total;  // a non-finite blob: no grid
+    bx0 = std::min(bx0, x), bx1 = std::max(bx1, x), by0 = std::min(by0, y), by1 = std::max(by1, y);
+  }
+  const double gx0 = bx0 - m, gy0 = by0 - m, w = bx1 - bx0 + 2 * m, h = by1 - by0 + 2 * m;
+  // square cells: at least the window (2m) and few enough for the cell budget
+  double cs = std::max(2.0 * m, std::sqrt(w * h / (double)kGridMaxCells));
+  int ncx = (int)std::ceil(w / cs), ncy = (int)std::ceil(h / cs);
+  while ((int64_t)ncx * ncy > kGridMaxCells) {
+    cs *= 1.0625;
+    ncx = (int)std::ceil(w / cs);
+    ncy = (int)std::ceil(h / cs);
+  }
+  ncx = std::max(1, ncx);
+  ncy = std::max(1, ncy);
+  const float inv_c = (float)(1.0 / cs), gx0f = (float)gx0, gy0f = (float)gy0;
+  auto crange = [&](double lo, double hi, float inv, float org, int n, int& c0, int& c1) {
+    const double f0 = (lo - (double)org) * (double)inv, f1 = (hi - (double)org) * (double)inv;
+    c0 = (int)std::max(0.0, std::min((double)(n - 1), std::floor(f0)));
+    c1 = (int)std::max(0.0, std::min((double)(n - 1), std::floor(f1)));
+  };
+  const int ncell = ncx * ncy;
+  std::vector<int32_t> count(ncell + 1, 0);
+  int nent = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    std::vector<int32_t> fill;
+    if (pass == 1) {
+      for (int c = 0; c < ncell; ++c) count[c + 1] += count[c];
+      fill.assign(count.begin(), count.end() - 1);
+    }
+    for (int i = 0; i < B; ++i) {
+      const double x = (double)(float)blobs[2 * i], y = (double)(float)blobs[2 * i + 1];
+      int cx0, cx1, cy0, cy1;
+      crange(x - m, x + m, inv_c, gx0f, ncx, cx0, cx1);
+      crange(y - m, y + m, inv_c, gy0f, ncy, cy0, cy1);
+      for (int cy = cy0; cy <= cy1; ++cy)
+        for (int cx = cx0; cx <= cx1; ++cx) {
+          const int c = cy * ncx + cx;
+          if (pass == 0) {
+            ++count[c + 1];
+            ++nent;
+          } else {
+            const int e = fill[c]++;
+            BlobXY<float>* gxy = (BlobXY<float>*)((unsigned char*)gh + sizeof(GridHdr) + align16((size_t)ncell * 4));
+            int32_t* gorig = (int32_t*)((unsigned char*)gxy + align16((size_t)(nent + 1) * 8));
+            gxy[e].x = (float)blobs[2 * i];
+            gxy[e].y = (float)blobs[2 * i + 1];
+            gorig[e] = i;
+          }
+        }
+    }
+    if (pass == 0 && nent > kGridMaxEntries) return total;  // too many entries: the x-buckets serve
+  }
+  uint32_t* cell = (uint32_t*)((unsigned char*)gh + sizeof(GridHdr));
+  for (int c = 0; c < ncell; ++c) cell[c] = (uint32_t)count[c] | ((uint32_t)(count[c + 1] - count[c]) << 16);
+  BlobXY<float>* gxy = (BlobXY<float>*)((unsigned char*)cell + align16((size_t)ncell * 4));
+  int32_t* gorig = (int32_t*)((unsigned char*)gxy + align16((size_t)(nent + 1) * 8));
+  gxy[nent].x = gxy[nent].y = 0.0f;  // the padding entry read by a masked second candidate
+  gorig[nent] = 0;
+  gh->inv_c = inv_c;
+  gh->gx0 = gx0f;
+  gh->gy0 = gy0f;
+  gh->fmaxx = (float)(ncx - 1);
+  gh->fmaxy = (float)(ncy - 1);
+  gh->gtolq = (float)tolq;
+  gh->ncx = ncx;
+  gh->ncell = ncell;
+  gh->nent = nent;
+  return BlobTable<T>::total_bytes(B, ncell, nent);
 }
 
 // block-wide copy of the table into LDS (16-byte words); callers barrier before use
@@ -1780,7 +1979,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   BlockPart* parts = slot ? part1 : part0;
   const int lane = lane_id(), wv = wave_id();
   int vb = (int)blockIdx.x;
-  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  copy_table(table, smem, (size_t)fa.tbytes);
   // raw state values of this block's particle (converted where they are used), so the loads of the next
   // block's particle can stay in flight across a whole block's arithmetic
   SP R[12];
@@ -2061,7 +2260,7 @@ __device__ __forceinline__ void propagate_weigh_block(
   const bool valid = n < fa.N;
   // table loads first: vmcnt retires in order, so the LDS copy then waits only for them while the
   // prior loads stay in flight across the barrier
-  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  copy_table(table, smem, (size_t)fa.tbytes);
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
   // written by the previous launch: the exit rule already fired (uniform), and this iteration's weight slot
@@ -2174,7 +2373,6 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   }
   const int first = __builtin_amdgcn_readfirstlane(hd->first_blk);
   const int nblk = __builtin_amdgcn_readfirstlane(hd->fa.nblk);
-  const int B = __builtin_amdgcn_readfirstlane(hd->fa.B);
   const unsigned char* tab = hd->table;
   uint16_t* bm = (uint16_t*)(dev + boff);
   for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
@@ -2182,7 +2380,7 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   if (to < tbytes) {
     gv4_t* src = (gv4_t*)(host + to);
     u32x4_t* dst = (u32x4_t*)(dev + to);
-    const int n4 = (int)(BlobTable<T>::bytes(B) / 16);
+    const int n4 = __builtin_amdgcn_readfirstlane(hd->fa.tbytes) / 16;
     for (int i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
   }
 }
@@ -2966,7 +3164,7 @@ __global__ __launch_bounds__(kBlock) void k_frame(
   const int lane = lane_id(), wv = wave_id();
   const int blk = blockIdx.x, g = blk / fa.gsz;
 
-  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  copy_table(table, smem, (size_t)fa.tbytes);
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
   const uint32_t gen_base = ((uint32_t)seq & 0xffffu) << 16;  // iteration release values of this frame
@@ -3261,7 +3459,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   const int lane = lane_id(), wv = wave_id();
   const int blk = blockIdx.x, g_own = blk / fa.gsz;
 
-  copy_table(table, smem, BlobTable<T>::bytes(fa.B));
+  copy_table(table, smem, (size_t)fa.tbytes);
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
   stage_consts(fa, sc);

@@ -105,6 +105,7 @@ struct pfmpe_ctx {
   unsigned char* d_bank = nullptr;   // staged tables of a whole stream, back to back
   std::vector<size_t> bank_off;      // byte offset of frame f's table
   std::vector<int32_t> bank_B;
+  std::vector<GridHdr> bank_grid;    // frame f's table grid header (host copy, for the kernel arguments)
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
@@ -358,7 +359,7 @@ template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
   static int iterate(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table, int iter) {
     const SP* prior = (const SP*)c->d_state[c->prior_idx];
-    const size_t lds = BlobTable<T>::lds_bytes(fa.B);
+    const size_t lds = BlobTable<T>::lds_bytes(fa.tbytes);
     uint32_t* gcount = c->d_counters;
     uint32_t* tcount = c->d_counters + c->max_grp;
     RET(ensure_prop(c));
@@ -450,7 +451,7 @@ struct Seq {
     *launched = false;
     const bool flat = c->fused == 2 && fa_in.nblk <= kFlatMaxGroups * kGroup && fa_in.gsz == kGroup && c->d_flat;
     const void* fn = flat ? (const void*)k_frame2<T, RNG, MAXM, PRUNE, SP> : (const void*)k_frame<T, RNG, MAXM, PRUNE, SP>;
-    const size_t lds = BlobTable<T>::lds_bytes(fa_in.B);
+    const size_t lds = BlobTable<T>::lds_bytes(fa_in.tbytes);
     auto key = std::make_pair(fn, lds);
     auto it = c->occ.find(key);
     if (it == c->occ.end()) {
@@ -616,7 +617,7 @@ struct Seq {
         x.seq = c->seq;
         x.first_blk = (int32_t)total;
         total += fa.nblk;
-        lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.B));
+        lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.tbytes));
         lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
       }
       const BatchLayout Lt = batch_layout<Desc>(na, total, tbytes);
@@ -689,8 +690,10 @@ template <typename T>
 FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
 
 template <typename T, int RNG, typename SP>
-int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
+int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table, size_t tbytes, const GridHdr& gh) {
   FrameArgsT<T> fa = build_args<T>(c, in);
+  fa.tbytes = (int32_t)tbytes;
+  fa.grid = grid_args<T>(gh, fa.B, (float)fa.tolq);
   for (int q = 0; q < 12; ++q) {  // fp16 state: anchors of the prior and of the new prior (current pose)
     fa.anc_in[q] = (T)c->anchor[c->prior_idx][q];
     fa.anc_out[q] = (T)in->current_pose[q];
@@ -734,9 +737,9 @@ int audit_batch(pfmpe_ctx* const* cs, int S, const FrameArgsT<T>* fas, const pfm
     if (in[s].bank_frame >= 0) {
       const size_t f = (size_t)in[s].bank_frame;
       if (!c->d_bank || f >= c->bank_B.size() || c->bank_B[f] != fa.B ||
-          c->bank_off[f] + BlobTable<T>::bytes(fa.B) > c->bank_off.back())
+          c->bank_off[f] + (size_t)fa.tbytes != c->bank_off[f + 1] || fa.tbytes < (int)BlobTable<T>::bytes(fa.B))
         return bad(s, "bank table");
-    } else if (toff[s] + BlobTable<T>::bytes(fa.B) > tbytes) {
+    } else if (toff[s] + (size_t)fa.tbytes > tbytes || fa.tbytes < (int)BlobTable<T>::bytes(fa.B)) {
       return bad(s, "host table");
     }
     first += fa.nblk;
@@ -756,6 +759,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   pfmpe_ctx* c0 = cs[0];
   std::vector<FrameArgsT<T>> fas(S);
   std::vector<size_t> toff(S, 0);
+  std::vector<std::vector<unsigned char>> hosttab(S);
   size_t tbytes = 0;
   int64_t total = 0;
   int maxM = 1;
@@ -766,9 +770,17 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
       fas[s].anc_in[q] = (T)c->anchor[c->prior_idx][q];
       fas[s].anc_out[q] = (T)in[s].current_pose[q];
     }
-    if (in[s].bank_frame < 0) {
+    if (in[s].bank_frame < 0) {  // host blobs: the table is built now (its size depends on the blobs)
+      hosttab[s].resize(BlobTable<T>::max_bytes());
+      fas[s].tbytes = (int32_t)build_blob_table_host<T>(in[s].blobs, in[s].B, (double)fas[s].tolq, hosttab[s].data());
+      fas[s].grid = grid_args<T>(*(const GridHdr*)(hosttab[s].data() + BlobTable<T>::off_grid(in[s].B)), in[s].B,
+                                 (float)fas[s].tolq);
       toff[s] = tbytes;
-      tbytes += (BlobTable<T>::bytes(in[s].B) + 255) / 256 * 256;
+      tbytes += ((size_t)fas[s].tbytes + 255) / 256 * 256;
+    } else {
+      const size_t f = (size_t)in[s].bank_frame;
+      fas[s].tbytes = (int32_t)(c->bank_off[f + 1] - c->bank_off[f]);
+      fas[s].grid = grid_args<T>(c->bank_grid[f], in[s].B, (float)fas[s].tolq);
     }
     total += fas[s].nblk;
     maxM = std::max(maxM, c->M);
@@ -804,7 +816,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     if (in[s].bank_frame >= 0) {
       tables[s] = c->d_bank + c->bank_off[in[s].bank_frame];
     } else {
-      build_blob_table_host<T>(in[s].blobs, in[s].B, c0->h_multi + toff[s]);
+      std::memcpy(c0->h_multi + toff[s], hosttab[s].data(), (size_t)fas[s].tbytes);
       tables[s] = c0->d_multi + toff[s];
     }
   }
@@ -921,7 +933,7 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
 
 
 #define PFMPE_DECLARE_INSTANCE(T, RNG, SP, EXT)                                                           \
-  EXT template int dispatch_m<T, RNG, SP>(pfmpe_ctx*, const pfmpe_frame_in*, const unsigned char*);        \
+  EXT template int dispatch_m<T, RNG, SP>(pfmpe_ctx*, const pfmpe_frame_in*, const unsigned char*, size_t, const GridHdr&);        \
   EXT template int regen_m<T, RNG, SP>(pfmpe_ctx*, int, const void*, double*);                            \
   EXT template int multi_m<T, RNG, SP>(pfmpe_ctx* const*, int, const pfmpe_frame_in*);
 

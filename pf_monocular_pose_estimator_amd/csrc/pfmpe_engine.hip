@@ -20,18 +20,19 @@ PFMPE_DECLARE_INSTANCE(float, kRngPhilox, __half, extern)
 namespace {
 using namespace pfmpe_impl;
 
-int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table) {
+int dispatch_step(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table, size_t tbytes,
+                  const GridHdr& gh) {
   const bool ref = c->params.rng_mode == PFMPE_RNG_REFERENCE;
   switch (c->state_dtype) {
     case PFMPE_STATE_F64:
-      return ref ? dispatch_m<double, kRngReference, double>(c, in, table)
-                 : dispatch_m<double, kRngPhilox, double>(c, in, table);
+      return ref ? dispatch_m<double, kRngReference, double>(c, in, table, tbytes, gh)
+                 : dispatch_m<double, kRngPhilox, double>(c, in, table, tbytes, gh);
     case PFMPE_STATE_F16:
-      return ref ? dispatch_m<float, kRngReference, __half>(c, in, table)
-                 : dispatch_m<float, kRngPhilox, __half>(c, in, table);
+      return ref ? dispatch_m<float, kRngReference, __half>(c, in, table, tbytes, gh)
+                 : dispatch_m<float, kRngPhilox, __half>(c, in, table, tbytes, gh);
     default:
-      return ref ? dispatch_m<float, kRngReference, float>(c, in, table)
-                 : dispatch_m<float, kRngPhilox, float>(c, in, table);
+      return ref ? dispatch_m<float, kRngReference, float>(c, in, table, tbytes, gh)
+                 : dispatch_m<float, kRngPhilox, float>(c, in, table, tbytes, gh);
   }
 }
 
@@ -67,14 +68,21 @@ void launch_export(pfmpe_ctx* c, int N, const double* anchor) {
 }
 
 
-size_t table_bytes(const pfmpe_ctx* c, int B) {
-  return c->state_dtype == PFMPE_STATE_F64 ? BlobTable<double>::bytes(B) : BlobTable<float>::bytes(B);
+// byte offset of a table's GridHdr
+size_t grid_off(const pfmpe_ctx* c, int B) {
+  return c->state_dtype == PFMPE_STATE_F64 ? BlobTable<double>::off_grid(B) : BlobTable<float>::off_grid(B);
 }
-void build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* dst) {
-  if (c->state_dtype == PFMPE_STATE_F64)
-    build_blob_table_host<double>(blobs, B, dst);
-  else
-    build_blob_table_host<float>(blobs, B, dst);
+// largest blob table of this context's type (base part at kMaxBlobs + the largest grid)
+size_t table_max_bytes(const pfmpe_ctx* c) {
+  return c->state_dtype == PFMPE_STATE_F64 ? BlobTable<double>::max_bytes() : BlobTable<float>::max_bytes();
+}
+// the frame's blob table for the context's current parameters (pruning half-window as build_args computes
+// it); returns its size
+size_t build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char* dst) {
+  const double tolq = c->state_dtype == PFMPE_STATE_F64 ? (c->params.tol_pf * (1.0 + 1e-3) + 1e-3)
+                                                        : (double)(float)(c->params.tol_pf * (1.0 + 1e-3) + 1e-3);
+  if (c->state_dtype == PFMPE_STATE_F64) return build_blob_table_host<double>(blobs, B, tolq, dst);
+  return build_blob_table_host<float>(blobs, B, tolq, dst);
 }
 
 
@@ -233,8 +241,8 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
     memset(c->h_rec, 0, sizeof(RecOut));
     c->h_out = new OutDev();
   }
-  ok &= hipMalloc((void**)&c->d_table, table_bytes(c, kMaxBlobs)) == hipSuccess;
-  ok &= hipHostMalloc((void**)&c->h_table, table_bytes(c, kMaxBlobs), hipHostMallocDefault) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_table, table_max_bytes(c)) == hipSuccess;
+  ok &= hipHostMalloc((void**)&c->h_table, table_max_bytes(c), hipHostMallocDefault) == hipSuccess;
   if (!ok) return bad(PFMPE_E_HIP);
   // Zeroed in the context's own stream and waited for: the stream is non-blocking, so a null-stream
   // hipMemset could still be in flight when the first frame's kernels read these words (freed memory of an
@@ -390,13 +398,17 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
   }
   c->bank_off.assign(nframes + 1, 0);
   c->bank_B.assign(nframes, 0);
+  // tables are built with the parameters current now (their grid's window); a frame stepped later with a
+  // wider tol_PF falls back to the x-buckets of the same table (column_minima checks the grid's window)
+  c->bank_grid.assign(nframes, GridHdr{});
+  std::vector<unsigned char> host, one(table_max_bytes(c));
   for (int f = 0; f < nframes; ++f) {
     c->bank_B[f] = offsets[f + 1] - offsets[f];
-    c->bank_off[f + 1] = c->bank_off[f] + table_bytes(c, c->bank_B[f]);
+    const size_t n = build_table(c, blobs + 2 * (size_t)offsets[f], c->bank_B[f], one.data());
+    host.insert(host.end(), one.begin(), one.begin() + n);
+    c->bank_off[f + 1] = c->bank_off[f] + n;
+    c->bank_grid[f] = *(const GridHdr*)(one.data() + grid_off(c, c->bank_B[f]));
   }
-  std::vector<unsigned char> host(c->bank_off[nframes]);
-  for (int f = 0; f < nframes; ++f)
-    build_table(c, blobs + 2 * (size_t)offsets[f], c->bank_B[f], host.data() + c->bank_off[f]);
   HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
   HIPCHK(c, hipMemcpyAsync(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));  // `host` goes out of scope; the frames read the bank in this stream
@@ -408,15 +420,20 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   RET(set_device(c));
   const unsigned char* table = c->d_table;
   const int B = in->B;
+  size_t tbytes = 0;
+  GridHdr gh{};
   if (in->bank_frame >= 0) {
     table = c->d_bank + c->bank_off[in->bank_frame];
+    tbytes = c->bank_off[in->bank_frame + 1] - c->bank_off[in->bank_frame];
+    gh = c->bank_grid[in->bank_frame];
   } else {
     // the x-bucketed table is built here, O(B), and travels in the same copy the blobs would
-    build_table(c, in->blobs, B, c->h_table);
-    HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, table_bytes(c, B), hipMemcpyHostToDevice, c->stream));
+    tbytes = build_table(c, in->blobs, B, c->h_table);
+    gh = *(const GridHdr*)(c->h_table + grid_off(c, B));
+    HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
-  const int rs = dispatch_step(c, in, table);
+  const int rs = dispatch_step(c, in, table, tbytes, gh);
   if (c->timing_now) {
     c->timing_now = false;
     if (rs == PFMPE_OK) RET(harvest_timing(c));
