@@ -62,6 +62,16 @@ constexpr int kPlanes = 12;            // r00 r01 r02 t0 r10 r11 r12 t1 r20 r21 
 
 enum : int { kRngReference = 0, kRngPhilox = 1 };
 
+// Marker-count buckets (pfmpe_ctx.hpp dispatch_m / multi_m): the per-particle loops are unrolled to MAXM slots.
+// The 5-slot bucket serves exactly M == 5 (the README object: C1, C2, C4, C5), so its "slot j holds a marker"
+// tests are compile-time true: no per-marker lane masks live across the streaming loops (they held SGPR pairs
+// spilled to VGPR lanes, a v_readlane pair per use).  The other buckets test j < M.
+constexpr int kExactM = 5;
+template <int MAXM>
+__host__ __device__ __forceinline__ bool marker_live(int j, int M) {
+  return MAXM == kExactM ? j < kExactM : j < M;
+}
+
 // ----------------------------------------------------------------------------- kernel arguments
 // Passed by value (kernarg segment -> scalar loads), pre-converted to the compute type T on the host.
 // The frame's 2D blob grid as kernel arguments (scalar registers, reloadable from the kernarg segment /
@@ -536,7 +546,7 @@ __device__ __forceinline__ void project_markers(const FrameArgsT<T>& fa, const L
   }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
-    if (j < fa.M) {
+    if (marker_live<MAXM>(j, fa.M)) {
       const T X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
       T p[3];
 #pragma unroll
@@ -647,7 +657,7 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
       for (int j = 0; j < MAXM; ++j) {
         float bd = INFINITY;
         int bo = 0;
-        if (j < M) {
+        if (marker_live<MAXM>(j, M)) {
           const int cx = (int)__builtin_amdgcn_fmed3f((u[j] - ga.gx0) * ga.inv_c, 0.0f, ga.fmaxx);
           const int cy = (int)__builtin_amdgcn_fmed3f((v[j] - ga.gy0) * ga.inv_c, 0.0f, ga.fmaxy);
           const uint32_t rec = cell[mad24(cy, ga.ncx, cx)];
@@ -684,7 +694,7 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
       uint64_t best = ((uint64_t)0x7f800000u << 32) | 0x7fffffffu;
-      if (j < M) {
+      if (marker_live<MAXM>(j, M)) {
         int c0 = 0, c1 = B;
         if (PRUNE) {
           const float flo = (u[j] - base_lo) * tb.inv_bw;
@@ -718,7 +728,7 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
   for (int j = 0; j < MAXM; ++j) {
     T best = inf_t<T>();
     int bc = -1;  // table position of the current minimum
-    if (j < M) {
+    if (marker_live<MAXM>(j, M)) {
       int c0 = 0, c1 = B;
       if (PRUNE) {
         c0 = tb.bstart[bucket_of(u[j] - fa.tolq, tb.xmin, tb.inv_bw, tb.nb)];
@@ -794,7 +804,7 @@ __device__ __forceinline__ T score_minima(const FrameArgsT<T>& fa, const T* m, c
   int kj[MAXM], kr[MAXM];
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
-    km[j] = j < M ? m[j] : inf_t<T>();
+    km[j] = marker_live<MAXM>(j, M) ? m[j] : inf_t<T>();
     kj[j] = j;
     kr[j] = r[j];
   }
@@ -2451,7 +2461,7 @@ __device__ __forceinline__ int pairs_from_minima(const FrameArgsT<T>& fa, const 
     int rj = 0;
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
-      mj = (lane == j && j < M) ? opaque(m[j]) : mj;
+      mj = (lane == j && marker_live<MAXM>(j, M)) ? opaque(m[j]) : mj;
       rj = lane == j ? opaque(r[j]) : rj;
     }
     int rank = 0;
@@ -3098,8 +3108,8 @@ __device__ __forceinline__ void resample_final_block(
   int r[MAXM];
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
-    m[j] = j < fa.M ? mk[j] : inf_t<T>();
-    r[j] = j < fa.M ? rk[j] : 0;
+    m[j] = marker_live<MAXM>(j, fa.M) ? mk[j] : inf_t<T>();
+    r[j] = marker_live<MAXM>(j, fa.M) ? rk[j] : 0;
   }
   const int np = pairs_from_minima<T, MAXM>(fa, tb, m, r, u0, v0, ccorr);  // wave 0 projected marker 0
   const uint32_t pl = payload_word<T>(Pc, ccorr, np);

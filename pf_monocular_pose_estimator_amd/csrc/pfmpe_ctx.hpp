@@ -700,7 +700,7 @@ int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* tabl
   }
   // marker capacity buckets: the per-particle loops are unrolled to MAXM (5: the 5-LED configs C1/C2/C4,
   // 12: C3)
-  if (fa.M <= 5) return Seq<T, RNG, 5, SP>::step(c, fa, table);
+  if (fa.M == kExactM) return Seq<T, RNG, kExactM, SP>::step(c, fa, table);  // the 5-slot bucket is exact (marker_live)
   if (fa.M <= 8) return Seq<T, RNG, 8, SP>::step(c, fa, table);
   if (fa.M <= 12) return Seq<T, RNG, 12, SP>::step(c, fa, table);
   return Seq<T, RNG, 16, SP>::step(c, fa, table);
@@ -763,8 +763,10 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   size_t tbytes = 0;
   int64_t total = 0;
   int maxM = 1;
+  bool all5 = true;  // every stream has exactly kExactM markers: the exact 5-slot bucket serves the batch
   for (int s = 0; s < S; ++s) {
     pfmpe_ctx* c = cs[s];
+    all5 = all5 && c->M == kExactM;
     fas[s] = build_args<T>(c, &in[s]);
     for (int q = 0; q < 12; ++q) {
       fas[s].anc_in[q] = (T)c->anchor[c->prior_idx][q];
@@ -821,8 +823,8 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     }
   }
   int rc;
-  if (maxM <= 5)
-    rc = Seq<T, RNG, 5, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
+  if (all5)
+    rc = Seq<T, RNG, kExactM, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
   else if (maxM <= 8)
     rc = Seq<T, RNG, 8, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
   else if (maxM <= 12)
