@@ -77,11 +77,19 @@ __host__ __device__ __forceinline__ bool marker_live(int j, int M) {
 // The frame's 2D blob grid as kernel arguments (scalar registers, reloadable from the kernarg segment /
 // stream descriptor instead of held in VGPRs): build_blob_table_host's GridHdr plus the byte offsets of the
 // grid's parts in the table; on = 0 when the table has no grid or one built for a narrower window.
+// one 2D-grid list entry of a blob table (build_blob_table_host): position and original index, one ds_read_b128
+struct alignas(16) GridEnt {
+  float x, y;
+  int32_t orig, pad;
+};
 struct GridArgs {
-  float inv_c, gx0, gy0, pad0;     // cell of (u, v): ((u - gx0) * inv_c, (v - gy0) * inv_c), clamped (square cells)
+  float inv_c, ox, oy, pad0;       // cell of (u, v): (fma(u, inv_c, ox), fma(v, inv_c, oy)), clamped, truncated;
+                                   // ox = -gx0 * inv_c (square cells)
   float fmaxx, fmaxy;              // ncx - 1, ncy - 1
   int32_t ncx, on;
-  int32_t cell_off, gxy_off, gorig_off, pad;  // table offsets: uint32 cell[], BlobXY<float> gxy[], int32 gorig[]
+  int32_t cell_off, ent_off;      // table offsets: uint32 cell[], GridEnt ent[]
+  int32_t b0fin;                  // blob 0 of the table is finite (set whether or not the grid is on)
+  int32_t dense;                  // most list entries sit in multi-blob cells: two entries per marker up front
 };
 
 template <typename T>
@@ -90,7 +98,8 @@ struct FrameArgsT {
   T markers[kMaxMarkers * 3];
   T K[9];
   T lo[6], hi[6];           // draw ranges angX angY angZ tX tY tZ (scaled by fac*), Philox stream
-  T rg[6];                  // hi - lo, rounded once on the host (the fp32 Philox draw is lo + u * rg)
+  T rgs[6];                 // (hi - lo) * 2^-21: hi - lo rounded once on the host, then scaled exactly (Philox draw
+                            // lo + u21 * (hi - lo) with u21 = v * 2^-21, computed as v * rgs: the same product)
   double dlo[6], dhi[6];    // the same in double, reference stream (draws are computed in double)
   double growth;            // 0.025
   T tol, tol_pf, tolq;      // score normaliser / acceptance gate / pruning half-window
@@ -121,7 +130,7 @@ struct LdsConst {
   T markers[kMaxMarkers * 3];
   T K[9];
   T lo[6], hi[6];
-  T rg[6];
+  T rgs[6];
 };
 
 // Per-frame control record.  All-zero is the valid "start of frame" state (zeroed at create, set_prior
@@ -249,7 +258,7 @@ __device__ __forceinline__ T inf_t() {
 template <typename T>
 __device__ __forceinline__ void stage_consts_from(const uint32_t* src, LdsConst<T>& sc) {
   static_assert(offsetof(FrameArgsT<T>, cur) == 0 && offsetof(FrameArgsT<T>, hi) == offsetof(LdsConst<T>, hi) &&
-                    offsetof(FrameArgsT<T>, rg) == offsetof(LdsConst<T>, rg),
+                    offsetof(FrameArgsT<T>, rgs) == offsetof(LdsConst<T>, rgs),
                 "LdsConst must mirror the head of FrameArgsT");
   static_assert(sizeof(LdsConst<T>) % 4 == 0, "dword copy");
   uint32_t* dst = (uint32_t*)&sc;
@@ -354,6 +363,59 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
   }
 }
 
+// Prefetch form (k_weigh_stream): the 12 raw plane words of particle n as 32-bit registers (fp16 values
+// zero-extended), loaded by every lane without a branch (a lane past N reads inside the planes or gets 0 from
+// the resource bound).  Raw halves kept as halves were packed in pairs by the compiler right after the loads
+// (v_perm), which waited for the prefetch at once; a branch around the loads made the next wait vmcnt(0).
+// fp64 planes (flat accesses) keep the guarded load.
+// fp16 planes: planes 2k and 2k + 1 share one register, filled by buffer_load_short_d16 / _d16_hi (each
+// writes its half and keeps the other), so the pair needs no packing instruction and no wait.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <typename SP>
+struct RawState {
+  SP v[12];
+};
+template <>
+struct RawState<__half> {
+  u16x2 p[6];
+};
+template <>
+struct RawState<float> {
+  uint32_t v[12];
+};
+template <typename SP>
+__device__ __forceinline__ void load_state_prefetch(const SP* __restrict__ base, int64_t ld, int n, bool want,
+                                                    RawState<SP>& R) {
+  if constexpr (BufPlanes<SP>::value) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
+    const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
+    if constexpr (sizeof(SP) == 2) {
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        u16x2 x = R.p[k];
+        x.x = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k) * ps, 0);
+        x.y = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k + 1) * ps, 0);
+        R.p[k] = x;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) R.v[q] = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)q * ps, 0);
+    }
+  } else {
+    if (want) load_state_raw<SP>(base, ld, n, R.v);
+  }
+}
+// StateIO::load of prefetched plane q
+template <typename T, typename SP>
+__device__ __forceinline__ T state_from_raw(const RawState<SP>& R, int q, T anchor) {
+  if constexpr (std::is_same<SP, __half>::value)
+    return StateIO<T, SP>::load(__ushort_as_half((q & 1) ? R.p[q >> 1].y : R.p[q >> 1].x), anchor);
+  else if constexpr (std::is_same<SP, float>::value)
+    return StateIO<T, SP>::load(__uint_as_float(R.v[q]), anchor);
+  else
+    return StateIO<T, SP>::load(R.v[q], anchor);
+}
+
 // prior particle n (SoA planes), loaded ahead of use so the loads overlap other work
 template <typename T, typename SP>
 __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __restrict__ prior, int n, T* A) {
@@ -425,12 +487,14 @@ __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsCons
     }
   } else {
     const Draws6 r = philox_motion6((uint32_t)n, (uint32_t)iter, fa.flo, fa.fhi, fa.key0, fa.key1);
-    const T g = (T)gd;
+    // draw = u21 * (hi - lo) + lo, u21 = v * 2^-21 (exact): v * rgs is the same product rounded once, so the
+    // conversion's scaling multiply is folded into the host constant
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const T u = u21_t<T>(r.v[q]);  // exact in either type
-      const T draw = u * sc.rg[q] + sc.lo[q];  // rg = hi - lo (host), the same value the device formed
-      d[q] = draw * g;
+    for (int q = 0; q < 6; ++q) d[q] = (T)r.v[q] * sc.rgs[q] + sc.lo[q];
+    if (iter >= 10) {  // wave-uniform: the growth factor 1 + growth * (iter / 10) is exactly 1 before iteration 10
+      const T g = (T)gd;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) d[q] = d[q] * g;
     }
   }
   T sa, ca, sb, cb, sz, cz;
@@ -648,44 +712,62 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
     if (PRUNE && ga.on) {  // wave-uniform (host: the table's grid covers this frame's window)
       // Grid walk: one cell list per marker (~1 candidate).  Its entries are in increasing original index, so
       // a strict "closer" test keeps the first (lowest-index) of equally close blobs, the key order above,
-      // and a NaN distance is never taken.  The first two entries are visited unconditionally (masked by the
-      // list length; a read past a short list stays inside the table), so the common path has no loop.
+      // and a NaN distance is never taken.  The list's first entry (the +inf sentinel for an empty cell) is
+      // taken without a test: bd = min(d, +inf) maps a NaN distance to +inf, and an empty cell leaves r = 0.
+      // Further entries are walked only when some lane's cell lists more than one blob (wave-uniform branch;
+      // the particles of a wave project each marker into one or two neighbouring cells, so it is rare).
+      // A non-finite first distance leaves r at that entry's index instead of 0: r is read only for a finite
+      // minimum within tol_PF (the gate), so no weight, pair or record changes.
       const uint32_t* cell = (const uint32_t*)(tb.base + ga.cell_off);
-      const BlobXY<float>* cxy = (const BlobXY<float>*)(tb.base + ga.gxy_off);
-      const int32_t* corig = (const int32_t*)(tb.base + ga.gorig_off);
+      const unsigned char* ents = tb.base + ga.ent_off;
+      const f32x2 ic = pk2(ga.inv_c, ga.inv_c), oc = pk2(ga.ox, ga.oy);
 #pragma unroll
       for (int j = 0; j < MAXM; ++j) {
         float bd = INFINITY;
         int bo = 0;
         if (marker_live<MAXM>(j, M)) {
-          const int cx = (int)__builtin_amdgcn_fmed3f((u[j] - ga.gx0) * ga.inv_c, 0.0f, ga.fmaxx);
-          const int cy = (int)__builtin_amdgcn_fmed3f((v[j] - ga.gy0) * ga.inv_c, 0.0f, ga.fmaxy);
-          const uint32_t rec = cell[mad24(cy, ga.ncx, cx)];
-          const int c0 = (int)(rec & 0xffffu), n = (int)(rec >> 16);
-          visited += n;
           const f32x2 uvj = pk2(u[j], v[j]);
-          auto visit = [&](BlobXY<float> p, int o, bool in) {
-            const f32x2 dd = pk2(p.x, p.y) - uvj;  // (dx, dy) in one v_pk_add_f32
+          const f32x2 f = pk_fma(uvj, ic, oc);  // both cell coordinates in one v_pk_fma_f32
+          const int cx = (int)__builtin_amdgcn_fmed3f(f.x, 0.0f, ga.fmaxx);
+          const int cy = (int)__builtin_amdgcn_fmed3f(f.y, 0.0f, ga.fmaxy);
+          const uint32_t rec = cell[mad24(cy, ga.ncx, cx)];
+          const GridEnt* e = (const GridEnt*)(ents + (rec & 0xffffu));
+          const int n = (int)(rec >> 16);
+          visited += n;
+          auto visit = [&](const GridEnt& ec, bool in) {
+            const f32x2 dd = pk2(ec.x, ec.y) - uvj;
             const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
             const bool take = in & (d < bd);
             bd = take ? d : bd;
-            bo = take ? o : bo;
+            bo = take ? ec.orig : bo;
           };
-          {
-            const BlobXY<float> pa = cxy[c0], pb = cxy[c0 + 1];
-            const int oa = corig[c0], ob = corig[c0 + 1];
-            visit(pa, oa, n > 0);
-            visit(pb, ob, n > 1);
+          int c1 = 1;
+          if (ga.dense) {  // wave-uniform: both first entries read together (one LDS round trip)
+            const GridEnt e0 = e[0], e1 = e[1];
+            const f32x2 dd = pk2(e0.x, e0.y) - uvj;
+            bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
+            bo = e0.orig;
+            visit(e1, n > 1);
+            c1 = 2;
+          } else {
+            const GridEnt e0 = e[0];
+            const f32x2 dd = pk2(e0.x, e0.y) - uvj;  // (dx, dy) in one v_pk_add_f32
+            bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
+            bo = e0.orig;
           }
-          for (int c = c0 + 2; c < c0 + n; c += 2) {  // rare: a cell with more than two blobs
-            const BlobXY<float> pa = cxy[c], pb = cxy[c + 1];
-            const int oa = corig[c], ob = corig[c + 1];
-            visit(pa, oa, true);
-            visit(pb, ob, c + 1 < c0 + n);
+          if (__ballot(n > c1)) {  // some lane's cell lists more entries (rare at 50 blobs)
+            // two entries per step, the second masked past the list end (its LDS read stays inside the table
+            // or its 16-B tail granule, BlobTable::lds_bytes)
+#pragma unroll 2
+            for (int c = c1; c < n; c += 2) {
+              const GridEnt ea = e[c], eb = e[c + 1];
+              visit(ea, true);
+              visit(eb, c + 1 < n);
+            }
           }
         }
         m[j] = bd;
-        r[j] = bo;  // 0 unless a candidate was taken (a finite distance), as the key form's r
+        r[j] = bo;
       }
       return visited;
     }
@@ -766,6 +848,15 @@ __device__ __forceinline__ bool nan_at_origin(T b0x, T b0y, T u0, T v0) {
   const T dx = b0x - u0, dy = b0y - v0;
   const T d = dx * dx + dy * dy;
   return d != d;
+}
+// The same test with the table's blob 0 finite (host flag, wave-uniform): (b0 - u0)^2 + (b0y - v0)^2 is NaN
+// exactly when u0 or v0 is NaN (an infinite difference squares to +inf and inf + inf = inf), one v_cmp_u; the
+// blob is read from the table header only when it is not finite.
+template <typename T>
+__device__ __forceinline__ bool nan_at_origin_tb(const FrameArgsT<T>& fa, const LdsBlobs<T>& tb, T u0, T v0) {
+  if (fa.grid.b0fin) return __builtin_isunordered(u0, v0);
+  const T* hdr = (const T*)tb.base;
+  return nan_at_origin(hdr[2], hdr[3], u0, v0);
 }
 
 // Extraction order = ascending (m_j, j): column minima are never NaN (they start at +inf and a NaN
@@ -1305,21 +1396,23 @@ __device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target, 
 //   base  hdr {T xmin, inv_bw, b0x, b0y} | int32 bstart[nb+1] | BlobXY<T> xy[B] | int32 orig[B]
 //         (the blobs grouped into nb = bucket_count(B) x-buckets, increasing original index within a bucket;
 //         every blob once: the linear scans of pose_pairs / k_resample_final and the fp64 pruned minima)
-//   grid  GridHdr | uint32 cell[ncell] (start | count << 16) | BlobXY<float> gxy[nent + 1] | int32 gorig[nent + 1]
+//   grid  GridHdr | uint32 cell[ncell] (byte offset of the list in ent[] | count << 16) | GridEnt ent[nent + 1]
 //         (fp32 tables: a 2D cell grid over the blobs' bounding box widened by the pruning half-window; cell c
 //         lists every blob whose +-tolq box (plus 0.01 px) overlaps it, so a marker's candidates are ONE
-//         cell's list.  ncell = 0: no grid, the x-buckets serve; fp64 tables and large B never build one)
+//         cell's list.  ent[0] is a sentinel {+inf, +inf, 0}: an empty cell points at it, so every query reads
+//         one entry without a test.  ncell = 0: no grid, the x-buckets serve; fp64 tables and large B never
+//         build one)
 __host__ __device__ constexpr size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 struct GridHdr {
   float inv_c, gx0, gy0, pad0;     // cell of (u, v): ((u - gx0) * inv_c, (v - gy0) * inv_c), clamped
   float fmaxx, fmaxy;              // ncx - 1, ncy - 1
   float gtolq;                     // half-window the lists were built for (>= the frame's tolq to be used)
   int32_t ncx, ncell, nent;        // columns, cells, list entries
-  int32_t pad[2];
+  int32_t b0fin, dense;            // blob 0 finite (every table, grid or not); GridArgs::dense
 };
 static_assert(sizeof(GridHdr) == 48, "grid header");
-constexpr int kGridMaxCells = 1024;   // cell records: 4 KB
-constexpr int kGridMaxEntries = 1024; // list entries: 12 KB (B up to ~400 blobs at 2-3 cells each)
+constexpr int kGridMaxCells = 2048;   // cell records: 8 KB
+constexpr int kGridMaxEntries = 1024; // list entries: 16 KB (B up to ~400 blobs at 2-3 cells each)
 template <typename T>
 struct BlobTable {
   static constexpr size_t off_bstart() { return align16(4 * sizeof(T)); }
@@ -1329,13 +1422,13 @@ struct BlobTable {
   static constexpr size_t bytes(int B) { return off_orig(B) + align16((size_t)B * 4); }
   static constexpr size_t off_grid(int B) { return bytes(B); }
   static constexpr size_t grid_bytes(int ncell, int nent) {
-    return sizeof(GridHdr) + align16((size_t)ncell * 4) + align16((size_t)(nent + 1) * 8) + align16((size_t)(nent + 1) * 4);
+    return sizeof(GridHdr) + align16((size_t)ncell * 4) + (size_t)(nent + 1) * sizeof(GridEnt);
   }
   // a table's total size: base + grid (the host builder returns it; FrameArgsT::tbytes carries it)
   static constexpr size_t total_bytes(int B, int ncell, int nent) { return bytes(B) + grid_bytes(ncell, nent); }
   static constexpr size_t max_bytes() { return total_bytes(kMaxBlobs, kGridMaxCells, kGridMaxEntries); }
   // LDS of the weighing kernels: the table plus one 16-B granule, so the masked second candidate of the
-  // fp32 column_minima step reads inside the allocation
+  // fp32 column_minima steps (x-buckets, grid lists) reads inside the allocation
   static constexpr size_t lds_bytes(size_t tbytes) { return tbytes + 16; }
 };
 
@@ -1345,7 +1438,7 @@ struct LdsBlobs {
   const BlobXY<T>* bxy;
   const int32_t* orig;
   const int32_t* bstart;  // nb + 1
-  T xmin, inv_bw, b0x, b0y;
+  T xmin, inv_bw;  // blob 0 (header words 2, 3): read where needed (nan_at_origin_tb)
   int nb;
 };
 
@@ -1356,8 +1449,6 @@ __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* 
   t.base = base;
   t.xmin = hdr[0];
   t.inv_bw = hdr[1];
-  t.b0x = hdr[2];
-  t.b0y = hdr[3];
   t.nb = bucket_count(B);
   t.bstart = (const int32_t*)(base + BlobTable<T>::off_bstart());
   t.bxy = (const BlobXY<T>*)(base + BlobTable<T>::off_xy(B));
@@ -1370,17 +1461,18 @@ __host__ __device__ __forceinline__ LdsBlobs<T> view_table(const unsigned char* 
 template <typename T>
 inline GridArgs grid_args(const GridHdr& gh, int B, float tolq) {
   GridArgs g{};
+  g.b0fin = gh.b0fin;
   g.on = (gh.ncell > 0 && gh.gtolq >= tolq) ? 1 : 0;
   if (!g.on) return g;
   g.inv_c = gh.inv_c;
-  g.gx0 = gh.gx0;
-  g.gy0 = gh.gy0;
+  g.ox = (float)(-(double)gh.gx0 * (double)gh.inv_c);  // build_blob_table_host's proof covers this rounding
+  g.oy = (float)(-(double)gh.gy0 * (double)gh.inv_c);
   g.fmaxx = gh.fmaxx;
   g.fmaxy = gh.fmaxy;
   g.ncx = gh.ncx;
+  g.dense = gh.dense;
   g.cell_off = (int32_t)(BlobTable<T>::off_grid(B) + sizeof(GridHdr));
-  g.gxy_off = g.cell_off + (int32_t)align16((size_t)gh.ncell * 4);
-  g.gorig_off = g.gxy_off + (int32_t)align16((size_t)(gh.nent + 1) * 8);
+  g.ent_off = g.cell_off + (int32_t)align16((size_t)gh.ncell * 4);
   return g;
 }
 
@@ -1421,18 +1513,20 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
     xy[pos].y = (T)blobs[2 * i + 1];
     orig[pos] = i;
   }
-  // ---- the grid (fp32 tables).  Device query: cell coordinate f = fl(fl(u - gx0) * inv_c), clamped by med3 to
-  // [0, ncx - 1], truncated.  Every blob within tol_PF of a query must be in the query's cell list:
+  // ---- the grid (fp32 tables).  Device query: cell coordinate f = fma(u, inv_c, ox), ox = fl(-gx0 * inv_c),
+  // clamped by med3 to [0, ncx - 1], truncated.  Every blob within tol_PF of a query must be in the query's
+  // cell list:
   //  * a blob is listed in every cell whose real-arithmetic interval [g(bx - m), g(bx + m)] it overlaps,
   //    g(x) = (x - gx0) * inv_c with the fp32 constants the device uses, m = tolq + 0.01 px;
-  //  * the device's f differs from g(u) by two roundings (coordinates < 2^11 px: a few 1e-4 px), far below
-  //    the m - tol_PF >= 0.01 px slack; a clamped query (outside the widened box) has no blob within tolq at
-  //    all, so whatever its cell lists, its minimum fails the gate;
+  //  * the device's f differs from g(u) by the rounding of ox and of the fma (cell coordinates < 2^7: a few
+  //    1e-6 cells, 1e-4 px), far below the m - tol_PF >= 0.01 px slack; a clamped query (outside the widened
+  //    box) has no blob within tolq at all, so whatever its cell lists, its minimum fails the gate;
   //  * every blob's own interval is clamped to the grid the same way.
   // Each list holds its blobs in increasing original index (the fill below runs over i), so the device's
   // strict "closer" comparison keeps the lowest index among equally close blobs: the reference's tie rule.
   GridHdr* gh = (GridHdr*)(dst + BlobTable<T>::off_grid(B));
   std::memset(gh, 0, sizeof(GridHdr));
+  gh->b0fin = (B > 0 && std::isfinite((double)hdr[2]) && std::isfinite((double)hdr[3])) ? 1 : 0;
   size_t total = BlobTable<T>::total_bytes(B, 0, 0);
   if (!std::is_same<T, float>::value || B == 0) return total;
   const double m = tolq + 0.01;
@@ -1480,23 +1574,27 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
             ++count[c + 1];
             ++nent;
           } else {
-            const int e = fill[c]++;
-            BlobXY<float>* gxy = (BlobXY<float>*)((unsigned char*)gh + sizeof(GridHdr) + align16((size_t)ncell * 4));
-            int32_t* gorig = (int32_t*)((unsigned char*)gxy + align16((size_t)(nent + 1) * 8));
-            gxy[e].x = (float)blobs[2 * i];
-            gxy[e].y = (float)blobs[2 * i + 1];
-            gorig[e] = i;
+            const int e = 1 + fill[c]++;  // ent[0]: the sentinel
+            GridEnt* ent = (GridEnt*)((unsigned char*)gh + sizeof(GridHdr) + align16((size_t)ncell * 4));
+            ent[e] = GridEnt{(float)blobs[2 * i], (float)blobs[2 * i + 1], i, 0};
           }
         }
     }
     if (pass == 0 && nent > kGridMaxEntries) return total;  // too many entries: the x-buckets serve
   }
   uint32_t* cell = (uint32_t*)((unsigned char*)gh + sizeof(GridHdr));
-  for (int c = 0; c < ncell; ++c) cell[c] = (uint32_t)count[c] | ((uint32_t)(count[c + 1] - count[c]) << 16);
-  BlobXY<float>* gxy = (BlobXY<float>*)((unsigned char*)cell + align16((size_t)ncell * 4));
-  int32_t* gorig = (int32_t*)((unsigned char*)gxy + align16((size_t)(nent + 1) * 8));
-  gxy[nent].x = gxy[nent].y = 0.0f;  // the padding entry read by a masked second candidate
-  gorig[nent] = 0;
+  for (int c = 0; c < ncell; ++c) {  // an empty cell points at the sentinel (byte offset 0)
+    const uint32_t n = (uint32_t)(count[c + 1] - count[c]);
+    cell[c] = (n ? (uint32_t)(1 + count[c]) * (uint32_t)sizeof(GridEnt) : 0u) | (n << 16);
+  }
+  GridEnt* ent = (GridEnt*)((unsigned char*)cell + align16((size_t)ncell * 4));
+  ent[0] = GridEnt{INFINITY, INFINITY, 0, 0};  // sentinel: distance +inf (NaN for a non-finite query), index 0
+  {  // dense lists (most entries in cells holding two or more blobs, e.g. 200 blobs): the device visits the
+     // first two entries of every list up front instead of one plus a wave-uniform check
+    int multi = 0;
+    for (int c = 0; c < ncell; ++c) multi += (count[c + 1] - count[c] > 1) ? count[c + 1] - count[c] : 0;
+    gh->dense = 2 * multi > nent ? 1 : 0;
+  }
   gh->inv_c = inv_c;
   gh->gx0 = gx0f;
   gh->gy0 = gy0f;
@@ -1816,7 +1914,7 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
   project_markers<T, MAXM>(fa, sc, P, u, v);
   if (st && threadIdx.x == 0) stamp_max(st, 28, rt_now() + (u[0] == (T)12345 ? 1 : 0));
   T w = (T)0;
-  if (fa.B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u[0], v[0])) {
+  if (fa.B > 0 && !nan_at_origin_tb(fa, tb, u[0], v[0])) {
     T m[MAXM];
     int r[MAXM];
     const int visited = column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
@@ -1847,9 +1945,95 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
 //    row_shr / row_bcast step adds a non-negative, lane-monotone addend, and rounding is monotone), so the
 //    maximum is lane 63's total and the minimum lane 0's value (valid lanes are a prefix of the wave).
 //    Only a wave holding a negative weight runs the two prefix max/min scans.
+// Wave totals through a butterfly instead of a scan (fp32 weighing passes, where only lane 63's inclusive sum is
+// needed).  quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror and row_mirror leave every lane of a quad /
+// half-row / row holding the same pairwise-tree value that wave_scan's row_shr 1/2/4/8 steps leave in the last lane
+// of each (lane 15 after shr8 = O1 + O0 = what lane 15 receives from lane 0 under row_mirror; fp addition is
+// commutative bit for bit), and the two row_bcast steps are wave_scan's own.  So lane 63 holds exactly wave_scan's
+// lane-63 value.  Every lane is a source in the first four steps (no fill value, no register init per step);
+// the bcast steps leave the rows they do not write holding garbage, which no caller reads.
+enum : int { kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141 };
+template <int CTRL, int RM = 0xf>
+__device__ __forceinline__ double dpp_any(double x) {
+  const uint64_t v = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, RM, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, RM, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_total_lane63(double x) {
+  x = x + dpp_any<kDppQuadXor1>(x);
+  x = x + dpp_any<kDppQuadXor2>(x);
+  x = x + dpp_any<kDppRowHalfMirror>(x);
+  x = x + dpp_any<kDppRowMirror>(x);
+  x = x + dpp_any<kDppBcast15, 0xa>(x);
+  x = x + dpp_any<kDppBcast31, 0xc>(x);
+  return x;
+}
+// max of a float over the wave as order-preserving integers (v_max_i32: no NaN canonicalisation per step; the
+// weights are never NaN); the result is the maximum's exact bits.  Rows are combined through lane reads.
+__device__ __forceinline__ int f32_sortable(float f) {
+  const int b = (int)__float_as_uint(f);
+  return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float wave_max_f32(float x) {
+  int k = f32_sortable(x);
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, false));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, false));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, false));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, false));
+  k = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
+          max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+  return __uint_as_float((uint32_t)(k ^ ((k >> 31) & 0x7fffffff)));  // the map is an involution
+}
+
 template <typename T>
 __device__ __forceinline__ void wave_weight_partials(T w, bool valid, int n, double& wi, double& rmx, double& rmn,
                                                      T& mx, int& ix, T& mn, int& in_) {
+  if constexpr (std::is_same<T, float>::value) {
+    // fp32 weighing passes: the wave total (lane 63 of wave_scan, bit for bit) through the butterfly, the max as
+    // integers; the inclusive prefix itself is formed only for a wave holding a negative weight (rare).
+    const double x = valid ? (double)w : 0.0;
+    const bool neg = __ballot(valid && w < 0.0f) != 0;  // wave-uniform
+    const uint64_t vmask = __ballot(valid);
+    mn = INFINITY;
+    in_ = 0x7fffffff;
+    if (!vmask) {  // no valid lane
+      wi = 0.0;
+      mx = -INFINITY;
+      ix = 0x7fffffff;
+      rmx = -INFINITY;
+      rmn = INFINITY;
+      return;
+    }
+    if (!neg) {
+      wi = wave_total_lane63(x);
+      mx = wave_max_f32(valid ? w : -INFINITY);
+      rmx = lane_value(wi, 63);
+      rmn = lane_value(x, 0);  // lane 0 is valid (valid lanes are a prefix of the wave)
+    } else {
+      wi = wave_incl_sum(x);
+      float mxs = valid ? w : -INFINITY;
+      mn = valid ? w : INFINITY;
+      rmx = valid ? wi : -INFINITY;
+      rmn = valid ? wi : INFINITY;
+      scan_steps([&](auto st) {
+        using S = decltype(st);
+        mxs = fmax_t(mxs, dpp<S::ctrl, S::rm>(mxs, -INFINITY));
+        mn = fmin_t(mn, dpp<S::ctrl, S::rm>(mn, INFINITY));
+        st_max<S>(rmx);
+        st_min<S>(rmn);
+      });
+      mx = lane_value(mxs, 63);
+      mn = lane_value(mn, 63);
+      const uint64_t bn = __ballot(valid && w == mn);
+      in_ = bn ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bn)) : 0x7fffffff;
+      rmx = lane_value(rmx, 63);
+      rmn = lane_value(rmn, 63);
+    }
+    const uint64_t bx = __ballot(valid && w == mx);
+    ix = bx ? __builtin_amdgcn_readlane(n, (int)__builtin_ctzll(bx)) : 0x7fffffff;
+    return;
+  }
   wi = valid ? (double)w : 0.0;
   mx = valid ? w : -inf_t<T>();
   const bool neg = __ballot(valid && w < (T)0) != 0;  // wave-uniform
@@ -1992,10 +2176,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   copy_table(table, smem, (size_t)fa.tbytes);
   // raw state values of this block's particle (converted where they are used), so the loads of the next
   // block's particle can stay in flight across a whole block's arithmetic
-  SP R[12];
+  RawState<SP> R{};
   {
     const int n = vb * kBlock + (int)threadIdx.x;
-    if (n < fa.N && n >= 2) load_state_raw<SP>(prior, fa.ld, n, R);
+    load_state_prefetch<SP>(prior, fa.ld, n, n < fa.N && n >= 2, R);
   }
   stage_consts(fa, sc);
   __syncthreads();  // table + constants visible
@@ -2006,8 +2190,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     const bool valid = n < fa.N;
     T A[12];
 #pragma unroll
-    for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(R[q], fa.anc_in[q]);
-    if (n + step < fa.N && n + step >= 2) load_state_raw<SP>(prior, fa.ld, n + step, R);  // next block's particle
+    for (int q = 0; q < 12; ++q) A[q] = state_from_raw<T, SP>(R, q, fa.anc_in[q]);
+    load_state_prefetch<SP>(prior, fa.ld, n + step, n + step < fa.N && n + step >= 2, R);  // next block's particle
     T w = (T)0, P[12];
     if (valid) w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
     if (valid) {
@@ -2454,7 +2638,7 @@ __device__ __forceinline__ int pairs_from_minima(const FrameArgsT<T>& fa, const 
   // holds key j (+inf past M, as in score_minima) and computes its rank; keys are distinct, so the ranks
   // are exactly the sorted positions.
   int np = 0;
-  if (B > 0 && !nan_at_origin(tb.b0x, tb.b0y, u0, v0)) {
+  if (B > 0 && !nan_at_origin_tb(fa, tb, u0, v0)) {
     const int M = fa.M;
     const int L = B < M ? B : M;
     T mj = inf_t<T>();
@@ -2900,7 +3084,9 @@ __device__ __forceinline__ void resample_phase(
 
 // ---- launch 2 of the two-launch path: stratified resampling + winner + frame record.  One block's work
 // (block `blk` of its stream), shared by k_resample and k_resample_multi.
-template <typename T, int RNG, int MAXM, typename SP, bool MULTI>
+// KEPT: every block of the launch has the kept propagated set (prop0 != null), so the regeneration path and its
+// registers are compiled out (the generic form, KEPT = false, tests prop0 at run time).
+template <typename T, int RNG, int MAXM, typename SP, bool MULTI, bool KEPT>
 __device__ __forceinline__ void resample_block(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post,
@@ -2914,8 +3100,13 @@ __device__ __forceinline__ void resample_block(
   const int g = blk / fa.gsz;
   const int n = blk * kBlock + threadIdx.x;
   const bool valid = n < fa.N;
+  // The frame constants go to LDS first (visible after block_incl_sum's barrier): their copy waits for its
+  // own loads (vmcnt retires in order), so issued before the weight / state loads it does not wait for them.
+  stage_consts_from(fa_words, sc);
   // Everything that does not depend on the control record is requested first (both weight slots: the
-  // kept one is known only from ctrl), so the loads overlap the ctrl read.
+  // kept one is known only from ctrl), so the loads overlap the ctrl read.  Loading only the kept slot after
+  // the ctrl read saves 4 B per particle of HBM reads but serialises the weight load behind it: C4 k_resample
+  // 163 -> 174 us (profiles/r03/ab_grid2.log), so both slots stay.
   T wt0 = (T)0, wt1 = (T)0;
   if (valid) {
     wt0 = w0[n];
@@ -2923,29 +3114,32 @@ __device__ __forceinline__ void resample_block(
   }
   const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
   const GroupScan gs = gscan[g];
+  const bool kept = KEPT || prop0 != nullptr;
   T A[12];
-  if (!prop0 && valid && n >= 2) load_prior(fa, prior, n, A);
+  if (!kept && valid && n >= 2) load_prior(fa, prior, n, A);
   const Ctrl c = MULTI ? load_ctrl_uniform(ctrl) : *ctrl;
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
   SP V[12];  // the kept iteration's stored propagated values (prop0)
-  if (prop0) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
+  if (kept) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
     const SP* src = c.kept_slot ? prop1 : prop0;
 #pragma unroll
     for (int q = 0; q < 12; ++q) V[q] = SP(0.0f);
-    if (valid) load_state_raw<SP>(src, fa.ld, n, V);
+    // buffer-resource planes: every lane loads (a lane past N reads inside the planes or gets 0 from the
+    // resource bound), so no branch: behind one, the weights' wait before the block scan became vmcnt(0) and
+    // also waited for these loads
+    if (BufPlanes<SP>::value || valid) load_state_raw<SP>(src, fa.ld, n, V);
     if constexpr (std::is_same<T, SP>::value) {  // fp16 rows are staged as they are (resample_phase RAWROW)
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = V[q];
     }
   }
-  stage_consts_from(fa_words, sc);  // visible after block_incl_sum's barrier
   const int slot = c.kept_slot;
   const double wd = valid ? (double)(slot ? wt1 : wt0) : 0.0;
   const BlockScan bs = slot ? bsb : bsa;  // by value: a reference to either local would force both to memory
   const LdsBlobs<T> tb = view_table<T>(table, fa.B);  // global memory (L2) in this launch
-  if (prop0)
+  if (kept)
     resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
                                               cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps,
                                               nullptr, blk, V);
@@ -2961,8 +3155,12 @@ __device__ __forceinline__ void resample_block(
 #ifndef PFMPE_RESAMPLE_MIN_WAVES
 #define PFMPE_RESAMPLE_MIN_WAVES 1
 #endif
-template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_MIN_WAVES))) void k_resample(
+// The kept-set variants (KEPT: no regeneration path, 60-66 VGPRs) take their own floor.
+#ifndef PFMPE_RESAMPLE_KEPT_MIN_WAVES
+#define PFMPE_RESAMPLE_KEPT_MIN_WAVES 8
+#endif
+template <typename T, int RNG, int MAXM, typename SP, bool KEPT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? PFMPE_RESAMPLE_KEPT_MIN_WAVES : PFMPE_RESAMPLE_MIN_WAVES))) void k_resample(
     const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
     SP* __restrict__ post, const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
@@ -2972,13 +3170,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RE
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
-  resample_block<T, RNG, MAXM, SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
+  resample_block<T, RNG, MAXM, SP, false, KEPT>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
                                    table, prior, post, w0, w1, bscan0, bscan1, gscan, cpart, cgroup, gcount, tcount,
                                    counts, cand, mlpose, out, seq, stamps, prop0, prop1, sc, rec, sh);
 }
 
-template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_MIN_WAVES))) void k_resample_multi(
+template <typename T, int RNG, int MAXM, typename SP, bool KEPT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? PFMPE_RESAMPLE_KEPT_MIN_WAVES : PFMPE_RESAMPLE_MIN_WAVES))) void k_resample_multi(
     const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
@@ -2987,7 +3185,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RE
   const int blk = batch_block(descs, bmap, S, &s);
   if (blk < 0) return;
   const StreamDesc<T, SP>& d = descs[s];
-  resample_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, blk, d.ctrl, d.table,
+  resample_block<T, RNG, MAXM, SP, true, KEPT>(d.fa, (const uint32_t*)&d.fa, blk, d.ctrl, d.table,
                                    d.prior, d.post, d.w0, d.w1, d.bscan0, d.bscan1, d.gscan, d.cpart, d.cgroup,
                                    d.gcount_r, d.tcount_r, d.counts, d.cand, d.mlpose, d.out, d.seq, nullptr, d.prop0,
                                    d.prop1, sc, rec, sh);

@@ -429,7 +429,9 @@ struct Seq {
     const int32_t seq = c->seq;
     const bool kept = c->keep_prop && c->d_prop[0];  // iterate() allocated them
     RET(launch_ext(c, PFMPE_K_RESAMPLE, [&] {
-      klaunch(c, k_resample<T, RNG, MAXM, SP>, dim3(fa.nblk), dim3(kBlock), 0, fa, c->d_ctrl, table,
+      // the kept-set variant compiles the regeneration path out (its registers spilled in the generic form)
+      auto k = kept ? k_resample<T, RNG, MAXM, SP, true> : k_resample<T, RNG, MAXM, SP, false>;
+      klaunch(c, k, dim3(fa.nblk), dim3(kBlock), 0, fa, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
@@ -582,6 +584,7 @@ struct Seq {
       Desc* hd = (Desc*)(h + L.doff);
       int64_t total = 0;
       size_t lds_w = 0, lds_f = 0;
+      bool all_kept = true;  // every stream has its kept propagated set: k_resample_multi<KEPT = true>
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
         const FrameArgsT<T>& fa = fas[act[i]];
@@ -607,6 +610,7 @@ struct Seq {
         const bool kept = c->keep_prop && c->d_prop[0];
         x.prop0 = kept ? (SP*)c->d_prop[0] : nullptr;
         x.prop1 = kept ? (SP*)c->d_prop[1] : nullptr;
+        all_kept = all_kept && kept;
         x.cpart = c->d_cpart;
         x.cgroup = c->d_cgroup;
         x.counts = c->record_counts ? c->d_counts : nullptr;
@@ -649,7 +653,10 @@ struct Seq {
         }));
       }
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
-        klaunch(c0, k_resample_multi<T, RNG, MAXM, SP>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
+        if (all_kept)
+          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
+        else
+          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, false>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
       }));
       RET(launch_ext(c0, PFMPE_K_FINAL, [&] {
         klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd);
@@ -888,7 +895,8 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   for (int q = 0; q < 6; ++q) {
     fa.lo[q] = (T)fa.dlo[q];
     fa.hi[q] = (T)fa.dhi[q];
-    fa.rg[q] = (T)(fa.hi[q] - fa.lo[q]);  // in T: the value the device formed before (bit-identical draws)
+    // hi - lo in T (the value the device formed before: bit-identical draws), times 2^-21 (exact)
+    fa.rgs[q] = (T)(fa.hi[q] - fa.lo[q]) * (T)0x1p-21;
   }
   fa.growth = p.growth;
   {  // fp32: every angle draw of the frame within kSmallAngle -> the short sincos polynomials (wave-uniform)

@@ -2,6 +2,9 @@
 #ifndef PFMPE_RESAMPLE_MIN_WAVES
 #define PFMPE_RESAMPLE_MIN_WAVES 6  // k_resample / k_resample_multi: 6 waves per SIMD (pf_kernels.hpp)
 #endif
+#ifndef PFMPE_RESAMPLE_KEPT_MIN_WAVES
+#define PFMPE_RESAMPLE_KEPT_MIN_WAVES 6  // the kept-set k_resample variants (pf_kernels.hpp)
+#endif
 #ifndef PFMPE_WEIGH_STREAM_MIN_WAVES
 #define PFMPE_WEIGH_STREAM_MIN_WAVES 6  // k_weigh_stream: 6 waves per SIMD (85 -> 80 VGPRs)
 #endif
