@@ -66,8 +66,9 @@ def parse():
     ap.add_argument("--prune", type=int, default=1, choices=[0, 1], help="exact blob pruning (1) or brute force (0)")
     ap.add_argument("--pmc", default="", help="PMC summary json (scripts/pmc_summary.py --json) of this same "
                     "workload; default profiles/pmc_<config>_n<N>.json when present")
-    ap.add_argument("--keep-prop", type=int, default=1, choices=[0, 1],
-                    help="two-launch path: store the propagated set (1) or regenerate it in k_resample (0)")
+    ap.add_argument("--keep-prop", type=int, default=-1, choices=[-1, 0, 1],
+                    help="two-launch path: store the propagated set (1) or regenerate it in k_resample (0); "
+                         "-1 = the library's default for the state type")
     ap.add_argument("--python-loop", action="store_true", help="one FFI call per frame instead of pfmpe_step_batch")
     ap.add_argument("--multi-sweep", default="",
                     help="after the timed region, also run S independent streams of the config per GPU as one "
@@ -252,7 +253,8 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
             eng.set_params(prm)
             eng.set_prior(st.prior())
             eng.set_option(pf.OPT_PRUNE, prune)
-            eng.set_option(pf.OPT_KEEP_PROPAGATED, keep_prop)
+            if keep_prop >= 0:
+                eng.set_option(pf.OPT_KEEP_PROPAGATED, keep_prop)
             eng.stage_blob_bank([f.blobs for f in st.frames])
             engs.append(eng)
             frames.append([eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs),
@@ -324,6 +326,8 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
         eng.set_prior(st.prior())
         eng.set_option(pf.OPT_FUSED, args.fused)
         eng.set_option(pf.OPT_PRUNE, args.prune)
+        if args.keep_prop >= 0:
+            if args.keep_prop >= 0:
         eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
         eng.stage_blob_bank([f.blobs for f in st.frames])
         frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
@@ -371,7 +375,8 @@ def main():
     eng.set_prior(st.prior())
     eng.set_option(pf.OPT_FUSED, args.fused)
     eng.set_option(pf.OPT_PRUNE, args.prune)
-    eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
+    if args.keep_prop >= 0:
+        eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
     if args.diag:
         eng.set_option(99, args.diag)
     eng.stage_blob_bank([f.blobs for f in st.frames])

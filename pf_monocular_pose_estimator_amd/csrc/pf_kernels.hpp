@@ -675,9 +675,8 @@ struct alignas(2 * sizeof(T)) BlobXY {
 // |bx-u| <= tolq (tolq >= tol_PF plus rounding slack) are visited.  Every blob within tol_PF lies in the
 // window, and a marker whose true minimum lies outside it fails the gate anyway, so accepted pairs,
 // penalties and the weight are unchanged; rejected markers only change their (unused) distance value.
-// (A 2D cell grid was measured slower: the extra cell arithmetic and nested row loop cost more than the
-// candidates it prunes.)  Candidates are read as packed (x, y); the original index is read only on an
-// exact distance tie (lowest index wins).
+// fp32 tables also carry a 2D cell grid (build_blob_table_host): a marker's candidates are then ONE cell's
+// list (a 2D window instead of an x-strip), walked by column_minima's grid branch.
 template <typename T>
 struct LdsBlobs;
 

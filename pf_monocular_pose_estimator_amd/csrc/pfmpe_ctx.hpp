@@ -139,7 +139,7 @@ struct pfmpe_ctx {
   // options
   bool record_counts = false;
   bool prune = true;
-  bool keep_prop = true;           // PFMPE_OPT_KEEP_PROPAGATED
+  bool keep_prop = true;           // PFMPE_OPT_KEEP_PROPAGATED (pfmpe_create: on for fp16 state only)
   int timing = 0;          // HIP-event sampling period in frames (0 = off)
   bool timing_now = false;  // this frame's launches are bracketed
   int64_t timing_frame = 0;

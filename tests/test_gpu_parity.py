@@ -523,7 +523,7 @@ def test_predict_roi_matches_oracle(state):
 @pytest.mark.parametrize("state", ["f64", "f32", "f16"])
 @pytest.mark.parametrize("occlude", [False, True])  # True: one LED hidden -> all 80 iterations, kept slot moves
 def test_kept_propagated_set_is_bit_identical(state, occlude):
-    """Two-launch path: gathering the stored propagated set (PFMPE_OPT_KEEP_PROPAGATED=1, default) and
+    """Two-launch path: gathering the stored propagated set (PFMPE_OPT_KEEP_PROPAGATED=1, the fp16 default) and
     regenerating it in k_resample (=0) give byte-identical frame records and new priors, frame after frame
     (the stored set follows the weights' slot, so a multi-iteration frame keeps the best iteration's set)."""
     N, M, B = 3000, 5, 30
