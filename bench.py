@@ -327,8 +327,7 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
         eng.set_option(pf.OPT_FUSED, args.fused)
         eng.set_option(pf.OPT_PRUNE, args.prune)
         if args.keep_prop >= 0:
-            if args.keep_prop >= 0:
-        eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
+            eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
         eng.stage_blob_bank([f.blobs for f in st.frames])
         frames = [eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs), bank_frame=f.index,
                                  dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index) for f in st.frames]
