@@ -314,8 +314,8 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *   PFMPE_OPT_KEEP_PROPAGATED [1|0] two-launch path: k_propagate_weigh stores each iteration's propagated
  *                                  set (two extra state buffers, allocated on first use) and k_resample
  *                                  gathers from it; 0 regenerates the kept set in k_resample instead.
- *                                  Results are bit-identical either way.  Default: 1 for PFMPE_STATE_F16,
- *                                  0 for fp32 / fp64 state (measured per state type)
+ *                                  Results are bit-identical either way.  Default 1; batched frames
+ *                                  (pfmpe_step_multi) use the stored set for fp16 state only (measured)
  *   PFMPE_OPT_WAIT_BOUND_US [2000000|>=1] bound of every in-launch wait of a one-launch frame.  A frame whose
  *                                  blocks are not all resident (other work holding CUs) is abandoned at the
  *                                  bound, redone with two launches (same result) and one-launch frames are

@@ -86,10 +86,10 @@ struct GridArgs {
   float inv_c, ox, oy, pad0;       // cell of (u, v): (fma(u, inv_c, ox), fma(v, inv_c, oy)), clamped, truncated;
                                    // ox = -gx0 * inv_c (square cells)
   float fmaxx, fmaxy;              // ncx - 1, ncy - 1
-  int32_t ncx, on;
+  int32_t ncx4, on;               // 4 * ncx: the cell row pitch in bytes
   int32_t cell_off, ent_off;      // table offsets: uint32 cell[], GridEnt ent[]
   int32_t b0fin;                  // blob 0 of the table is finite (set whether or not the grid is on)
-  int32_t dense;                  // most list entries sit in multi-blob cells: two entries per marker up front
+  int32_t pad2;
 };
 
 template <typename T>
@@ -717,7 +717,7 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
       // the particles of a wave project each marker into one or two neighbouring cells, so it is rare).
       // A non-finite first distance leaves r at that entry's index instead of 0: r is read only for a finite
       // minimum within tol_PF (the gate), so no weight, pair or record changes.
-      const uint32_t* cell = (const uint32_t*)(tb.base + ga.cell_off);
+      const unsigned char* cells = tb.base + ga.cell_off;
       const unsigned char* ents = tb.base + ga.ent_off;
       const f32x2 ic = pk2(ga.inv_c, ga.inv_c), oc = pk2(ga.ox, ga.oy);
 #pragma unroll
@@ -729,7 +729,8 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
           const f32x2 f = pk_fma(uvj, ic, oc);  // both cell coordinates in one v_pk_fma_f32
           const int cx = (int)__builtin_amdgcn_fmed3f(f.x, 0.0f, ga.fmaxx);
           const int cy = (int)__builtin_amdgcn_fmed3f(f.y, 0.0f, ga.fmaxy);
-          const uint32_t rec = cell[mad24(cy, ga.ncx, cx)];
+          // byte offset cy * 4 ncx + 4 cx (the row pitch scaled on the host)
+          const uint32_t rec = *(const uint32_t*)(cells + mad24(cy, ga.ncx4, cx << 2));
           const GridEnt* e = (const GridEnt*)(ents + (rec & 0xffffu));
           const int n = (int)(rec >> 16);
           visited += n;
@@ -740,21 +741,18 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
             bd = take ? d : bd;
             bo = take ? ec.orig : bo;
           };
-          int c1 = 1;
-          if (ga.dense) {  // wave-uniform: both first entries read together (one LDS round trip)
-            const GridEnt e0 = e[0], e1 = e[1];
-            const f32x2 dd = pk2(e0.x, e0.y) - uvj;
-            bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
-            bo = e0.orig;
-            visit(e1, n > 1);
-            c1 = 2;
-          } else {
+          // The 12 / 16-marker buckets (C3: 200 blobs, clustered, most lists longer than one) read the first
+          // two entries together; the exact 5-marker bucket (50 blobs) reads one and walks further entries only
+          // when some lane of the wave needs them.
+          constexpr int c1 = MAXM > kExactM ? 2 : 1;
+          {
             const GridEnt e0 = e[0];
             const f32x2 dd = pk2(e0.x, e0.y) - uvj;  // (dx, dy) in one v_pk_add_f32
             bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
             bo = e0.orig;
+            if constexpr (c1 == 2) visit(e[1], n > 1);
           }
-          if (__ballot(n > c1)) {  // some lane's cell lists more entries (rare at 50 blobs)
+          if (__builtin_amdgcn_ballot_w64(n > c1)) {  // some lane's list has more entries (rare at 50 blobs)
             // two entries per step, the second masked past the list end (its LDS read stays inside the table
             // or its 16-B tail granule, BlobTable::lds_bytes)
 #pragma unroll 2
@@ -1053,7 +1051,25 @@ __device__ __forceinline__ V wave_scan(V x, V id, Op op) {
   x = op(x, dpp<kDppBcast31, 0xc>(x, id));
   return x;
 }
-__device__ __forceinline__ double wave_incl_sum(double v) { return wave_scan(v, 0.0, OpSum()); }
+// Sum scan of doubles: the four row_shr steps read 0 (bound_ctrl) from a lane outside the row, which is the
+// sum's identity (+0.0 is all-zero bits), so they need no fill register; the two row_bcast steps write only
+// some rows and keep the fill.  Bit-identical to wave_scan(v, 0.0, OpSum()).
+template <int CTRL>
+__device__ __forceinline__ double dpp_zf(double x) {
+  const uint64_t v = (uint64_t)__double_as_longlong(x);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xf, 0xf, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xf, 0xf, true);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double wave_incl_sum(double x) {
+  x = x + dpp_zf<kDppRowShr1>(x);
+  x = x + dpp_zf<kDppRowShr2>(x);
+  x = x + dpp_zf<kDppRowShr4>(x);
+  x = x + dpp_zf<kDppRowShr8>(x);
+  x = x + dpp<kDppBcast15, 0xa>(x, 0.0);
+  x = x + dpp<kDppBcast31, 0xc>(x, 0.0);
+  return x;
+}
 __device__ __forceinline__ double wave_incl_max(double v) { return wave_scan(v, -(double)INFINITY, OpMax()); }
 __device__ __forceinline__ double wave_incl_min(double v) { return wave_scan(v, (double)INFINITY, OpMin()); }
 __device__ __forceinline__ double wave_max(double v) { return lane_value(wave_incl_max(v), 63); }
@@ -1407,7 +1423,7 @@ struct GridHdr {
   float fmaxx, fmaxy;              // ncx - 1, ncy - 1
   float gtolq;                     // half-window the lists were built for (>= the frame's tolq to be used)
   int32_t ncx, ncell, nent;        // columns, cells, list entries
-  int32_t b0fin, dense;            // blob 0 finite (every table, grid or not); GridArgs::dense
+  int32_t b0fin, pad;              // blob 0 finite (every table, grid or not)
 };
 static_assert(sizeof(GridHdr) == 48, "grid header");
 constexpr int kGridMaxCells = 2048;   // cell records: 8 KB
@@ -1468,8 +1484,7 @@ inline GridArgs grid_args(const GridHdr& gh, int B, float tolq) {
   g.oy = (float)(-(double)gh.gy0 * (double)gh.inv_c);
   g.fmaxx = gh.fmaxx;
   g.fmaxy = gh.fmaxy;
-  g.ncx = gh.ncx;
-  g.dense = gh.dense;
+  g.ncx4 = 4 * gh.ncx;
   g.cell_off = (int32_t)(BlobTable<T>::off_grid(B) + sizeof(GridHdr));
   g.ent_off = g.cell_off + (int32_t)align16((size_t)gh.ncell * 4);
   return g;
@@ -1588,12 +1603,7 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
   }
   GridEnt* ent = (GridEnt*)((unsigned char*)cell + align16((size_t)ncell * 4));
   ent[0] = GridEnt{INFINITY, INFINITY, 0, 0};  // sentinel: distance +inf (NaN for a non-finite query), index 0
-  {  // dense lists (most entries in cells holding two or more blobs, e.g. 200 blobs): the device visits the
-     // first two entries of every list up front instead of one plus a wave-uniform check
-    int multi = 0;
-    for (int c = 0; c < ncell; ++c) multi += (count[c + 1] - count[c] > 1) ? count[c + 1] - count[c] : 0;
-    gh->dense = 2 * multi > nent ? 1 : 0;
-  }
+
   gh->inv_c = inv_c;
   gh->gx0 = gx0f;
   gh->gy0 = gy0f;
@@ -2904,9 +2914,24 @@ __device__ __forceinline__ void resample_phase(
   }
 
   {  // block max count, first index (winner candidates)
-    int cv = valid ? cntn : -1;
-    int ci = valid ? n : 0x7fffffff;
-    wave_argmax(cv, ci);
+    int cv, ci;
+    if (N < (1 << 23)) {  // wave-uniform: (count, index) as ONE int key, count * 256 + (255 - thread), whose max
+                          // is the max count at its lowest index; integer max needs no canonicalising, and the
+                          // rows are combined through four lane reads
+      int k = valid ? cntn * 256 + (255 - (int)threadIdx.x) : -1;
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, false));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, false));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, false));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, false));
+      k = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
+              max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+      cv = k < 0 ? -1 : k >> 8;
+      ci = k < 0 ? 0x7fffffff : blk * kBlock + 255 - (k & 255);
+    } else {
+      cv = valid ? cntn : -1;
+      ci = valid ? n : 0x7fffffff;
+      wave_argmax(cv, ci);
+    }
     if (lane == 0) {
       sh.c[wv] = cv;
       sh.ci[wv] = ci;

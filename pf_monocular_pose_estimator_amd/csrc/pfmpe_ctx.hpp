@@ -139,7 +139,7 @@ struct pfmpe_ctx {
   // options
   bool record_counts = false;
   bool prune = true;
-  bool keep_prop = true;           // PFMPE_OPT_KEEP_PROPAGATED (pfmpe_create: on for fp16 state only)
+  bool keep_prop = true;           // PFMPE_OPT_KEEP_PROPAGATED (batched fp32 / fp64 frames regenerate: step_multi)
   int timing = 0;          // HIP-event sampling period in frames (0 = off)
   bool timing_now = false;  // this frame's launches are bracketed
   int64_t timing_frame = 0;
@@ -607,7 +607,9 @@ struct Seq {
         x.tcount_w = c->d_counters + c->max_grp;
         x.gcount_r = c->d_counters + c->max_grp + 1;
         x.tcount_r = c->d_counters + 2 * c->max_grp + 1;
-        const bool kept = c->keep_prop && c->d_prop[0];
+        // the stored set pays in batches only for fp16 state (round-3 A/B, DESIGN.md §4.2: 8 x C5 batches 5-8 %
+        // faster regenerating, 32 x C2 even); the choice changes no result
+        const bool kept = c->keep_prop && c->d_prop[0] && std::is_same<SP, __half>::value;
         x.prop0 = kept ? (SP*)c->d_prop[0] : nullptr;
         x.prop1 = kept ? (SP*)c->d_prop[1] : nullptr;
         all_kept = all_kept && kept;

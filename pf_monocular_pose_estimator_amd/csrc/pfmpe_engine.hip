@@ -195,9 +195,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   c->es = state_dtype == PFMPE_STATE_F64 ? 8 : (state_dtype == PFMPE_STATE_F16 ? 2 : 4);
   c->ws = state_dtype == PFMPE_STATE_F64 ? 8 : 4;
   c->ld = ((int64_t)max_particles + 63) / 64 * 64;
-  // PFMPE_OPT_KEEP_PROPAGATED default by state type (round-3 A/B): the fp16 set wins (C4
-  // 402-410 -> 371-376 us/frame); with fp32 state regenerating is even (C3, C5) or better (8 x C5 batches)
-  c->keep_prop = state_dtype == PFMPE_STATE_F16;
+
   c->max_blk = (max_particles + kBlock - 1) / kBlock;
   // fp32 / fp16 planes are addressed through one 32-bit buffer resource per state buffer
   // (pf_kernels.hpp BufPlanes): 12 planes must stay below 4 GiB (89M fp32 / 178M fp16 particles)
