@@ -363,6 +363,23 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
   }
 }
 
+// fp16 planes, particle k from six words holding planes (2j, 2j + 1) in their (low, high) halves: the high half
+// goes out through buffer_store_short_d16_hi, so no word is shifted first (the compiler does not select the
+// _d16_hi form for a store of x >> 16).  A vector store; the "memory" clobber keeps it ordered with the
+// compiler's own memory operations.
+__device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base, int64_t ld, int k, const uint32_t* w) {
+  const __amdgpu_buffer_rsrc_t r = plane_rsrc((const __half*)base, ld);
+  const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(__half));
+  const uint32_t voff = (uint32_t)k * 2u;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[j], r, voff, (uint32_t)(2 * j) * ps, 0);
+    asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(w[j]), "v"(voff), "s"(r),
+                 "s"((uint32_t)(2 * j + 1) * ps)
+                 : "memory");
+  }
+}
+
 // Prefetch form (k_weigh_stream): the 12 raw plane words of particle n as 32-bit registers (fp16 values
 // zero-extended), loaded by every lane without a branch (a lane past N reads inside the planes or gets 0 from
 // the resource bound).  Raw halves kept as halves were packed in pairs by the compiler right after the loads
@@ -1218,7 +1235,7 @@ __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters,
     const U32x4 o = philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
     U = u53(o.x, o.y);
   }
-  return (double)k + U;
+  return (double)(int32_t)k + U;  // 0 <= k <= N < 2^31: one v_cvt_f64_i32 (exact)
 }
 
 // r_k <= x, decided exactly without the fp64 division in all but a vanishing band.  With a = fl(k + U_k) and
@@ -2842,7 +2859,7 @@ __device__ __forceinline__ void resample_phase(
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, RecOut* __restrict__ out, int32_t seq,
-    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk, const SP* raw_in = nullptr) {
+    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk, const RawState<SP>* raw_in = nullptr) {
   constexpr bool INLAUNCH = MODE != 0;
   // fp16 stored set (RAW): the wave stages its kept particles' stored values as they are (12 halves, 24 B a
   // row) and the scatter copies them out unchanged, no widening / narrowing (raw_in: the lane's values)
@@ -2915,7 +2932,9 @@ __device__ __forceinline__ void resample_phase(
 
   {  // block max count, first index (winner candidates)
     int cv, ci;
-    if (N < (1 << 23)) {  // wave-uniform: (count, index) as ONE int key, count * 256 + (255 - thread), whose max
+    // wave-uniform: every count of the wave below 2^23 (always at N < 2^23; at larger N all but degenerate frames)
+    if (N < (1 << 23) || __ballot(valid && cntn >= (1 << 23)) == 0) {
+                          // (count, index) as ONE int key, count * 256 + (255 - thread), whose max
                           // is the max count at its lowest index; integer max needs no canonicalising, and the
                           // rows are combined through four lane reads
       int k = valid ? cntn * 256 + (255 - (int)threadIdx.x) : -1;
@@ -2966,13 +2985,10 @@ __device__ __forceinline__ void resample_phase(
   auto& rows = sh.rows[wv];
   uint2* rraw = (uint2*)&rows[0];  // RAWROW: three 8-B words per row
   if constexpr (RAWROW) {
-    uint32_t wd6[6];
 #pragma unroll
-    for (int j = 0; j < 6; ++j)
-      wd6[j] = (uint32_t)__builtin_bit_cast(uint16_t, raw_in[2 * j]) |
-               ((uint32_t)__builtin_bit_cast(uint16_t, raw_in[2 * j + 1]) << 16);
-#pragma unroll
-    for (int j = 0; j < 3; ++j) rraw[3 * lane + j] = make_uint2(wd6[2 * j], wd6[2 * j + 1]);
+    for (int j = 0; j < 3; ++j)
+      rraw[3 * lane + j] = make_uint2(__builtin_bit_cast(uint32_t, raw_in->p[2 * j]),
+                                      __builtin_bit_cast(uint32_t, raw_in->p[2 * j + 1]));
   } else {
 #pragma unroll
     for (int q = 0; q < 12; ++q) rows[lane].q[q] = P[q];  // also read by wave 0 for the block candidate
@@ -2988,28 +3004,28 @@ __device__ __forceinline__ void resample_phase(
       if (e > a && d >= 0 && d < 64) map[d] = lane;
       wave_lds_sync();
       int own = map[lane];
-      own = wave_scan(own, -1, OpMaxI());
+      own = wave_scan(own, INT_MIN, OpMaxI());  // INT_MIN fill: each step folds into one v_max_i32_dpp
       own = own > carry ? own : carry;
       carry = lane_value(own, 63);
       const int k = base + lane;
       wave_lds_sync();  // rows (before the loop) and this chunk's map reads are done before the next clear
       if (k < we) {
-        SP v[12];
         if constexpr (RAWROW) {
+          uint32_t w6[6];
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const uint2 x = rraw[3 * own + j];
-            v[4 * j + 0] = __builtin_bit_cast(SP, (uint16_t)(x.x & 0xffffu));
-            v[4 * j + 1] = __builtin_bit_cast(SP, (uint16_t)(x.x >> 16));
-            v[4 * j + 2] = __builtin_bit_cast(SP, (uint16_t)(x.y & 0xffffu));
-            v[4 * j + 3] = __builtin_bit_cast(SP, (uint16_t)(x.y >> 16));
+            w6[2 * j] = x.x;
+            w6[2 * j + 1] = x.y;
           }
+          store_state_words_f16(post, fa.ld, k, w6);
         } else {
+          SP v[12];
           const auto& row = rows[own];
 #pragma unroll
           for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
+          store_state_raw<SP>(post, fa.ld, k, v);
         }
-        store_state_raw<SP>(post, fa.ld, k, v);
       }
     }
   }
@@ -3145,16 +3161,22 @@ __device__ __forceinline__ void resample_block(
   // speculative launch of an unfinished frame, or the re-init branch (PE:707-719): nothing to resample;
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
-  SP V[12];  // the kept iteration's stored propagated values (prop0)
-  if (kept) {  // the kept iteration's stored propagated set: gathered as raw state values, no regeneration
+  // the kept iteration's stored propagated set, gathered as raw state values (no regeneration).  fp16: planes
+  // 2j and 2j + 1 land in the two halves of word j (buffer_load_short_d16 / _d16_hi), which is the row layout
+  // resample_phase stages, so the words need no packing instruction
+  RawState<SP> KR{};
+  if (kept) {
     const SP* src = c.kept_slot ? prop1 : prop0;
-#pragma unroll
-    for (int q = 0; q < 12; ++q) V[q] = SP(0.0f);
     // buffer-resource planes: every lane loads (a lane past N reads inside the planes or gets 0 from the
     // resource bound), so no branch: behind one, the weights' wait before the block scan became vmcnt(0) and
     // also waited for these loads
-    if (BufPlanes<SP>::value || valid) load_state_raw<SP>(src, fa.ld, n, V);
-    if constexpr (std::is_same<T, SP>::value) {  // fp16 rows are staged as they are (resample_phase RAWROW)
+    if constexpr (std::is_same<SP, __half>::value) {
+      load_state_prefetch<SP>(src, fa.ld, n, true, KR);
+    } else {
+      SP V[12];
+#pragma unroll
+      for (int q = 0; q < 12; ++q) V[q] = SP(0.0f);
+      if (BufPlanes<SP>::value || valid) load_state_raw<SP>(src, fa.ld, n, V);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = V[q];
     }
@@ -3166,7 +3188,7 @@ __device__ __forceinline__ void resample_block(
   if (kept)
     resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
                                               cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps,
-                                              nullptr, blk, V);
+                                              nullptr, blk, &KR);
   else
     resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
                                         mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk);

@@ -268,7 +268,15 @@ inline void klaunch(pfmpe_ctx* c, void (*kernel)(KArgs...), dim3 grid, dim3 bloc
   }
 }
 
+// Brackets are harvested lazily: a timed PF frame leaves its event pairs pending (no stream synchronize on the
+// frame path, which had added a host round trip to every sampled frame: at --steps 20 one frame in two), and
+// they are read here, when the pool holds kHarvestPairs of them, at pfmpe_get_kernel_stats, or after the
+// host-synchronous entries (ROI, read-backs, initialisation, detector).  Every bracket is recorded on c->stream,
+// so waiting for the last one's end event completes them all.
+constexpr size_t kHarvestPairs = 256;
 inline int harvest_timing(pfmpe_ctx* c) {
+  if (c->ev_used == 0) return PFMPE_OK;
+  HIPCHK(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].b));
   for (size_t i = 0; i < c->ev_used; ++i) {
     float ms = 0.f;
     HIPCHK(c, hipEventElapsedTime(&ms, c->ev_pool[i].a, c->ev_pool[i].b));
@@ -443,7 +451,6 @@ struct Seq {
                          table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0);
     }));
     RET(wait_frame(c));
-    if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));  // end events must have completed
     return PFMPE_OK;
   }
   // the whole frame as one launch, if every block can be resident at once: k_frame2 (flat hand-offs,
@@ -528,7 +535,6 @@ struct Seq {
       if (flat) c->flat_base_w += (uint32_t)o.iters * (uint32_t)a.nblk;
       if (o.resampled) c->flat_base_c += (uint32_t)a.nblk;
     }
-    if (c->timing_now) HIPCHK(c, hipStreamSynchronize(c->stream));
     return PFMPE_OK;
   }
 
@@ -679,7 +685,6 @@ struct Seq {
       act.swap(next);
       nb = round == 0 ? 1 : std::min(nb * 2, 16);
     }
-    if (c0->timing_now) HIPCHK(c0, hipStreamSynchronize(c0->stream));  // the brackets' end events completed
     for (int s = 0; s < S; ++s) {
       cs[s]->last_shape = PFMPE_SHAPE_TWO_LAUNCH;
       last_args<T>(cs[s]) = fas[s];

@@ -435,11 +435,9 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
   const int rs = dispatch_step(c, in, table, tbytes, gh);
-  if (c->timing_now) {
-    c->timing_now = false;
-    if (rs == PFMPE_OK) RET(harvest_timing(c));
-    c->ev_used = 0;
-  }
+  c->timing_now = false;
+  if (rs != PFMPE_OK) c->ev_used = 0;  // a failed frame's brackets are dropped
+  else if (c->ev_used >= kHarvestPairs) RET(harvest_timing(c));  // pending brackets: harvest_timing
   RET(rs);
   take_step(c, in, out);
   return PFMPE_OK;
@@ -476,11 +474,9 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
     default:
       rs = ref ? multi_m<float, kRngReference, float>(ctxs, S, in) : multi_m<float, kRngPhilox, float>(ctxs, S, in);
   }
-  if (c0->timing_now) {
-    c0->timing_now = false;
-    if (rs == PFMPE_OK) RET(harvest_timing(c0));
-    c0->ev_used = 0;
-  }
+  c0->timing_now = false;
+  if (rs != PFMPE_OK) c0->ev_used = 0;
+  else if (c0->ev_used >= kHarvestPairs) RET(harvest_timing(c0));
   RET(rs);
   for (int s = 0; s < S; ++s) {
     take_step(ctxs[s], &in[s], &out[s]);
@@ -581,7 +577,7 @@ int pfmpe_predict_roi(pfmpe_ctx* c, const pfmpe_roi_in* in, pfmpe_roi_out* out) 
   double bb[4];
   HIPCHK(c, hipMemcpyAsync(bb, c->d_roi, sizeof(bb), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->ev_used = 0;
+  RET(harvest_timing(c));
   // + the markers at predicted_pose_ (PE:1049-1052)
   for (int m = 0; m < c->M; ++m) {
     double uv[2];
@@ -635,7 +631,7 @@ int pfmpe_get_particles(pfmpe_ctx* c, int which, double* out) {
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, c->d_xfer, (size_t)N * 12 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  c->ev_used = 0;
+  RET(harvest_timing(c));
   return PFMPE_OK;
 }
 
@@ -698,6 +694,10 @@ int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
 
 int pfmpe_get_kernel_stats(pfmpe_ctx* c, int kernel, int64_t* launches, double* total_ms) {
   if (!c || kernel < 0 || kernel >= PFMPE_K_COUNT) return PFMPE_E_ARG;
+  if (c->ev_used) {  // pending brackets of timed frames
+    HIPCHK(c, hipSetDevice(c->device));
+    RET(harvest_timing(c));
+  }
   if (launches) *launches = c->k_launches[kernel];
   if (total_ms) *total_ms = c->k_ms[kernel];
   return PFMPE_OK;
@@ -718,6 +718,11 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
 
 int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
   if (!c) return PFMPE_E_ARG;
+  if (c->ev_used) {  // pending brackets belong to the statistics being reset
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].b));  // before their events are recorded again
+    c->ev_used = 0;
+  }
   for (int k = 0; k < PFMPE_K_COUNT; ++k) {
     c->k_launches[k] = 0;
     c->k_ms[k] = 0;
