@@ -289,6 +289,8 @@ __device__ __forceinline__ void compose(const T* A, const T* B, T* C) {
   }
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed fp32 pairs (v_pk_* forms)
+
 // Particle state storage S for compute type T: S == T (fp32 / fp64 planes), or fp16 planes holding
 // deltas to the set's anchor pose (PFMPE_STATE_F16, fp32 compute): 24 B per particle.
 template <typename T, typename SP>
@@ -444,6 +446,19 @@ __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __
 // particle k of a state buffer from its pose P (quantised against the anchor `anc` for fp16 state)
 template <typename T, typename SP>
 __device__ __forceinline__ void store_pose(SP* __restrict__ dst, int64_t ld, int k, const T* P, const T* anc) {
+  if constexpr (std::is_same<SP, __half>::value && std::is_same<T, float>::value) {
+    // fp16 deltas two planes at a time: one v_pk_add_f32 (the same fp32 subtractions) and one v_cvt_pk_f16_f32
+    // (round to nearest even, as __float2half) per pair, then the pair's halves as planes 2j / 2j + 1
+    typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+    uint32_t w[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const f32x2 d = f32x2{P[2 * j], P[2 * j + 1]} - f32x2{anc[2 * j], anc[2 * j + 1]};
+      w[j] = __builtin_bit_cast(uint32_t, __builtin_convertvector(d, f16x2));
+    }
+    store_state_words_f16(dst, ld, k, w);
+    return;
+  }
   SP v[12];
 #pragma unroll
   for (int q = 0; q < 12; ++q) v[q] = StateIO<T, SP>::store(P[q], anc[q]);
@@ -991,6 +1006,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// the same, as an SGPR (block sizes are multiples of 64): a loop over the earlier waves then has a scalar trip
+// count instead of a per-wave v_cndmask chain.  (Used where that pays: as the general wave_id it moved the
+// weighing pass's register allocation for the worse.)
+__device__ __forceinline__ int wave_id_u() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 // All wave-level scans and reductions run on DPP lane moves (no LDS, no ds_bpermute): row_shr 1/2/4/8
 // builds the inclusive scan inside each 16-lane row, row_bcast:15 / row_bcast:31 carry row totals
@@ -1166,9 +1185,9 @@ __device__ __forceinline__ void block_incl_sum(double v, double& incl, double* s
   if (lane_id() == 63) sh[wave_id()] = wi;
   __syncthreads();
   double pre = 0.0;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w)
-    if (w < wave_id()) pre = pre + sh[w];
+  const int wv = wave_id_u();
+#pragma clang loop unroll(disable)
+  for (int w = 0; w < wv; ++w) pre = pre + sh[w];  // a scalar trip count: no per-wave select chain
   incl = pre + wi;
 }
 
@@ -2901,7 +2920,9 @@ __device__ __forceinline__ void resample_phase(
   if (lane == 63) sh.max[wv] = rm;
   __syncthreads();
   double pm = rin;
-  for (int w = 0; w < wv; ++w) pm = sh.max[w] > pm ? sh.max[w] : pm;
+  const int wvu = wave_id_u();
+#pragma clang loop unroll(disable)
+  for (int w = 0; w < wvu; ++w) pm = sh.max[w] > pm ? sh.max[w] : pm;
   const double R = rm > pm ? rm : pm;
   const int hi = valid ? (int)count_targets<T, RNG>(fa, iters, R) : N;
   if (lane == 63) sh.hi[wv] = hi;
