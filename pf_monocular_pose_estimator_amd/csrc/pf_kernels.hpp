@@ -368,7 +368,7 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
 // fp16 planes, particle k from six words holding planes (2j, 2j + 1) in their (low, high) halves: the high half
 // goes out through buffer_store_short_d16_hi, so no word is shifted first (the compiler does not select the
 // _d16_hi form for a store of x >> 16).  A vector store; the "memory" clobber keeps it ordered with the
-// compiler's own memory operations.
+// compiler's own memory operations, and it carries its own VALU-SGPR-write -> VMEM wait states (below).
 __device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base, int64_t ld, int k, const uint32_t* w) {
   const __amdgpu_buffer_rsrc_t r = plane_rsrc((const __half*)base, ld);
   const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(__half));
@@ -376,7 +376,10 @@ __device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base,
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)w[j], r, voff, (uint32_t)(2 * j) * ps, 0);
-    asm volatile("buffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(w[j]), "v"(voff), "s"(r),
+    // s_nop 4 first: the compiler's hazard recognizer does not look inside inline asm, and the soffset /
+    // resource SGPRs may have just been written by a VALU (v_readlane of a spilled SGPR), which a VMEM
+    // instruction may read only 5 wait states later; without it the store used the stale offset
+    asm volatile("s_nop 4\n\tbuffer_store_short_d16_hi %0, %1, %2, %3 offen" ::"v"(w[j]), "v"(voff), "s"(r),
                  "s"((uint32_t)(2 * j + 1) * ps)
                  : "memory");
   }
@@ -524,6 +527,9 @@ __device__ __forceinline__ void propagate(const FrameArgsT<T>& fa, const LdsCons
 #pragma unroll
     for (int q = 0; q < 6; ++q) d[q] = (T)r.v[q] * sc.rgs[q] + sc.lo[q];
     if (iter >= 10) {  // wave-uniform: the growth factor 1 + growth * (iter / 10) is exactly 1 before iteration 10
+      // (the empty asm keeps this a scalar branch: if-converted, every frame paid the six products and six
+      // v_cndmask selects)
+      asm volatile("");
       const T g = (T)gd;
 #pragma unroll
       for (int q = 0; q < 6; ++q) d[q] = d[q] * g;
@@ -2210,7 +2216,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
                                                          SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
-  __shared__ WeighLds sh;
+  __shared__ WeighLds shb[2];  // wave partials, alternating by loop step (one barrier per block, below)
   if (ctrl->done) return;  // the exit rule already fired (uniform)
   const int slot = ctrl->cur_slot;
   T* wout = slot ? w1 : w0;
@@ -2230,7 +2236,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   __syncthreads();  // table + constants visible
   const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
   const int step = (int)gridDim.x * kBlock;
-  for (; vb < fa.nblk; vb += (int)gridDim.x) {
+  for (int step_i = 0; vb < fa.nblk; vb += (int)gridDim.x, ++step_i) {
+    WeighLds& sh = shb[step_i & 1];
     const int n = vb * kBlock + (int)threadIdx.x;
     const bool valid = n < fa.N;
     T A[12];
@@ -2281,7 +2288,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
       q.argmin = bin;
       parts[vb] = q;
     }
-    __syncthreads();  // sh is reused by the next block
+    // no second barrier: the other waves go on to the next block while thread 0 combines.  The next step
+    // writes the other buffer, and the step after it writes this one only after passing the next step's
+    // barrier, which thread 0 reaches only after this combine.
   }
 }
 
