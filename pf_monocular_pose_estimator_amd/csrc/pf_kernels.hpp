@@ -338,10 +338,39 @@ __device__ __forceinline__ void buf_st(__half v, __amdgpu_buffer_rsrc_t r, uint3
   __builtin_amdgcn_raw_buffer_store_b16(__half_as_ushort(v), r, voff, soff, 0);
 }
 
+// fp16 state layout (PFMPE_F16_PAIRS, default 1): planes 2j and 2j + 1 interleaved as ONE plane of 32-bit pairs,
+// element (q, n) at half index (q >> 1) * 2 ld + 2 n + (q & 1).  Every fp16 state access is then a 4-byte
+// access per lane (6 instead of 12 VMEM instructions per particle, 256 B per wave instruction), and the pair is
+// the register layout the kernels already use (RawState<__half>, store_state_words_f16).  0 keeps 12 planes of
+// halves (A/B).  fp32 / fp64 planes are unchanged.
+#ifndef PFMPE_F16_PAIRS
+#define PFMPE_F16_PAIRS 1
+#endif
+template <typename SP>
+__host__ __device__ __forceinline__ constexpr bool f16_pairs() {
+  return std::is_same<SP, __half>::value && PFMPE_F16_PAIRS != 0;
+}
+template <typename SP>
+__host__ __device__ __forceinline__ int64_t plane_index(int q, int64_t n, int64_t ld) {
+  if constexpr (f16_pairs<SP>())
+    return (int64_t)(q >> 1) * 2 * ld + 2 * n + (q & 1);
+  else
+    return (int64_t)q * ld + n;
+}
+
 // the 12 state values of particle n of a state buffer (raw SP values, no anchor / conversion)
 template <typename SP>
 __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int64_t ld, int n, SP* v) {
-  if constexpr (BufPlanes<SP>::value) {
+  if constexpr (f16_pairs<SP>()) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
+    const uint32_t pps = (uint32_t)(ld * 4);
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)p * pps, 0);
+      v[2 * p] = __ushort_as_half((unsigned short)(w & 0xffffu));
+      v[2 * p + 1] = __ushort_as_half((unsigned short)(w >> 16));
+    }
+  } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
 #pragma unroll
@@ -354,7 +383,15 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
 // store 12 raw state values as particle k
 template <typename SP>
 __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t ld, int k, const SP* v) {
-  if constexpr (BufPlanes<SP>::value) {
+  if constexpr (f16_pairs<SP>()) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
+    const uint32_t pps = (uint32_t)(ld * 4);
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      const uint32_t w = (uint32_t)__half_as_ushort(v[2 * p]) | ((uint32_t)__half_as_ushort(v[2 * p + 1]) << 16);
+      __builtin_amdgcn_raw_buffer_store_b32(w, r, (uint32_t)k * 4u, (uint32_t)p * pps, 0);
+    }
+  } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
 #pragma unroll
@@ -371,6 +408,12 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
 // compiler's own memory operations, and it carries its own VALU-SGPR-write -> VMEM wait states (below).
 __device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base, int64_t ld, int k, const uint32_t* w) {
   const __amdgpu_buffer_rsrc_t r = plane_rsrc((const __half*)base, ld);
+  if constexpr (f16_pairs<__half>()) {  // the words are the layout: one dword store each
+    const uint32_t pps = (uint32_t)(ld * 4);
+#pragma unroll
+    for (int j = 0; j < 6; ++j) __builtin_amdgcn_raw_buffer_store_b32(w[j], r, (uint32_t)k * 4u, (uint32_t)j * pps, 0);
+    return;
+  }
   const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(__half));
   const uint32_t voff = (uint32_t)k * 2u;
 #pragma unroll
@@ -390,8 +433,8 @@ __device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base,
 // the resource bound).  Raw halves kept as halves were packed in pairs by the compiler right after the loads
 // (v_perm), which waited for the prefetch at once; a branch around the loads made the next wait vmcnt(0).
 // fp64 planes (flat accesses) keep the guarded load.
-// fp16 planes: planes 2k and 2k + 1 share one register, filled by buffer_load_short_d16 / _d16_hi (each
-// writes its half and keeps the other), so the pair needs no packing instruction and no wait.
+// fp16 planes: planes 2k and 2k + 1 share one register: one dword load from the pair plane (PFMPE_F16_PAIRS),
+// or buffer_load_short_d16 / _d16_hi into its two halves (12 half planes), so the pair needs no packing.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 template <typename SP>
 struct RawState {
@@ -411,7 +454,11 @@ __device__ __forceinline__ void load_state_prefetch(const SP* __restrict__ base,
   if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
-    if constexpr (sizeof(SP) == 2) {
+    if constexpr (f16_pairs<SP>()) {  // one dword per pair plane
+#pragma unroll
+      for (int k = 0; k < 6; ++k)
+        R.p[k] = __builtin_bit_cast(u16x2, __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)k * (uint32_t)(ld * 4), 0));
+    } else if constexpr (sizeof(SP) == 2) {
 #pragma unroll
       for (int k = 0; k < 6; ++k) {
         u16x2 x = R.p[k];
@@ -2216,7 +2263,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
                                                          SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
-  __shared__ WeighLds shb[2];  // wave partials, alternating by loop step (one barrier per block, below)
+  __shared__ WeighLds sh;
   if (ctrl->done) return;  // the exit rule already fired (uniform)
   const int slot = ctrl->cur_slot;
   T* wout = slot ? w1 : w0;
@@ -2236,8 +2283,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   __syncthreads();  // table + constants visible
   const LdsBlobs<T> tb = view_table<T>(smem, fa.B);
   const int step = (int)gridDim.x * kBlock;
-  for (int step_i = 0; vb < fa.nblk; vb += (int)gridDim.x, ++step_i) {
-    WeighLds& sh = shb[step_i & 1];
+  for (; vb < fa.nblk; vb += (int)gridDim.x) {
     const int n = vb * kBlock + (int)threadIdx.x;
     const bool valid = n < fa.N;
     T A[12];
@@ -2288,9 +2334,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
       q.argmin = bin;
       parts[vb] = q;
     }
-    // no second barrier: the other waves go on to the next block while thread 0 combines.  The next step
-    // writes the other buffer, and the step after it writes this one only after passing the next step's
-    // barrier, which thread 0 reaches only after this combine.
+    __syncthreads();  // sh is reused by the next block (one barrier per block with double-buffered partials
+                      // measured 2-4 us slower at C4, profiles/r03/ab_r03b.log)
   }
 }
 
@@ -3928,7 +3973,7 @@ __global__ void k_import(const double* __restrict__ poses, SP* __restrict__ st, 
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   for (int q = 0; q < 12; ++q)
-    st[(int64_t)q * ld + n] = StateIO<T, SP>::store((T)poses[12 * (int64_t)n + q], anchor.v[q]);
+    st[plane_index<SP>(q, n, ld)] = StateIO<T, SP>::store((T)poses[12 * (int64_t)n + q], anchor.v[q]);
 }
 template <typename T, typename SP>
 __global__ void k_export(const SP* __restrict__ st, double* __restrict__ poses, int N, int64_t ld,
@@ -3936,7 +3981,7 @@ __global__ void k_export(const SP* __restrict__ st, double* __restrict__ poses, 
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   for (int q = 0; q < 12; ++q)
-    poses[12 * (int64_t)n + q] = (double)StateIO<T, SP>::load(st[(int64_t)q * ld + n], anchor.v[q]);
+    poses[12 * (int64_t)n + q] = (double)StateIO<T, SP>::load(st[plane_index<SP>(q, n, ld)], anchor.v[q]);
 }
 template <typename T, int RNG, typename SP>
 __global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int kept_iter, const SP* __restrict__ prior,
@@ -3971,7 +4016,7 @@ __global__ __launch_bounds__(kBlock) void k_roi(const RoiArgs ra, const SP* __re
     double A[12], X[12], P[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q)
-      A[q] = (double)StateIO<T, SP>::load(prior[(int64_t)q * ra.ld + n], (T)ra.anchor[q]);
+      A[q] = (double)StateIO<T, SP>::load(prior[plane_index<SP>(q, n, ra.ld)], (T)ra.anchor[q]);
     compose(ra.cam, A, X);   // camMoveInv * newPoseEstimation[j]
     compose(X, ra.predm, P); // ... * predictionMatrix
     double Q[12];
