@@ -343,16 +343,27 @@ __device__ __forceinline__ void buf_st(__half v, __amdgpu_buffer_rsrc_t r, uint3
 // access per lane (6 instead of 12 VMEM instructions per particle, 256 B per wave instruction), and the pair is
 // the register layout the kernels already use (RawState<__half>, store_state_words_f16).  0 keeps 12 planes of
 // halves (A/B).  fp32 / fp64 planes are unchanged.
+// fp32 state likewise (PFMPE_F32_PAIRS): 6 planes of 64-bit pairs, one dwordx2 per lane and pair.  Default 0:
+// measured C5 k_resample -2 us but C3 k_propagate_weigh +1..5 us, and the one batched run that faulted this
+// round (an aperture violation in k_resample_multi, 16 C2 streams as two concurrent batches) used it
+// (profiles/r03/multi_fault_f32pairs_abm_new.log); not kept until that is explained.
 #ifndef PFMPE_F16_PAIRS
 #define PFMPE_F16_PAIRS 1
+#endif
+#ifndef PFMPE_F32_PAIRS
+#define PFMPE_F32_PAIRS 0
 #endif
 template <typename SP>
 __host__ __device__ __forceinline__ constexpr bool f16_pairs() {
   return std::is_same<SP, __half>::value && PFMPE_F16_PAIRS != 0;
 }
 template <typename SP>
+__host__ __device__ __forceinline__ constexpr bool f32_pairs() {
+  return std::is_same<SP, float>::value && PFMPE_F32_PAIRS != 0;
+}
+template <typename SP>
 __host__ __device__ __forceinline__ int64_t plane_index(int q, int64_t n, int64_t ld) {
-  if constexpr (f16_pairs<SP>())
+  if constexpr (f16_pairs<SP>() || f32_pairs<SP>())
     return (int64_t)(q >> 1) * 2 * ld + 2 * n + (q & 1);
   else
     return (int64_t)q * ld + n;
@@ -369,6 +380,15 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
       const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)p * pps, 0);
       v[2 * p] = __ushort_as_half((unsigned short)(w & 0xffffu));
       v[2 * p + 1] = __ushort_as_half((unsigned short)(w >> 16));
+    }
+  } else if constexpr (f32_pairs<SP>()) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
+    const uint32_t pps = (uint32_t)(ld * 8);
+#pragma unroll
+    for (int p = 0; p < 6; ++p) {
+      const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)n * 8u, (uint32_t)p * pps, 0);
+      v[2 * p] = __uint_as_float(w[0]);
+      v[2 * p + 1] = __uint_as_float(w[1]);
     }
   } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
@@ -391,6 +411,14 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
       const uint32_t w = (uint32_t)__half_as_ushort(v[2 * p]) | ((uint32_t)__half_as_ushort(v[2 * p + 1]) << 16);
       __builtin_amdgcn_raw_buffer_store_b32(w, r, (uint32_t)k * 4u, (uint32_t)p * pps, 0);
     }
+  } else if constexpr (f32_pairs<SP>()) {
+    const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
+    const uint32_t pps = (uint32_t)(ld * 8);
+    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{__float_as_uint(v[2 * p]), __float_as_uint(v[2 * p + 1])}, r,
+                                            (uint32_t)k * 8u, (uint32_t)p * pps, 0);
   } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
@@ -429,8 +457,10 @@ __device__ __forceinline__ void store_state_words_f16(__half* __restrict__ base,
 }
 
 // Prefetch form (k_weigh_stream): the 12 raw plane words of particle n as 32-bit registers (fp16 values
-// zero-extended), loaded by every lane without a branch (a lane past N reads inside the planes or gets 0 from
-// the resource bound).  Raw halves kept as halves were packed in pairs by the compiler right after the loads
+// zero-extended), loaded by every lane without a branch.  The caller clamps the particle index into [0, N) for
+// lanes past N (in_planes): the buffer resource's range check covers the VGPR offset only, not the plane offset
+// in soffset, so an unclamped lane past ld read past the end of the allocation (up to a plane beyond it for the
+// streaming pass's last prefetch); the loaded values of such lanes are never used.  Raw halves kept as halves were packed in pairs by the compiler right after the loads
 // (v_perm), which waited for the prefetch at once; a branch around the loads made the next wait vmcnt(0).
 // fp64 planes (flat accesses) keep the guarded load.
 // fp16 planes: planes 2k and 2k + 1 share one register: one dword load from the pair plane (PFMPE_F16_PAIRS),
@@ -448,6 +478,8 @@ template <>
 struct RawState<float> {
   uint32_t v[12];
 };
+// a particle index every plane access may use: n for n < N, else N - 1 (one v_min; see load_state_prefetch)
+__device__ __forceinline__ int in_planes(int n, int N) { return (int)min((unsigned)n, (unsigned)(N - 1)); }
 template <typename SP>
 __device__ __forceinline__ void load_state_prefetch(const SP* __restrict__ base, int64_t ld, int n, bool want,
                                                     RawState<SP>& R) {
@@ -465,6 +497,13 @@ __device__ __forceinline__ void load_state_prefetch(const SP* __restrict__ base,
         x.x = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k) * ps, 0);
         x.y = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k + 1) * ps, 0);
         R.p[k] = x;
+      }
+    } else if constexpr (f32_pairs<SP>()) {  // one dwordx2 per pair plane
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)n * 8u, (uint32_t)k * (uint32_t)(ld * 8), 0);
+        R.v[2 * k] = w[0];
+        R.v[2 * k + 1] = w[1];
       }
     } else {
 #pragma unroll
@@ -1789,6 +1828,10 @@ __device__ __forceinline__ GroupScan load_gscan_wt(const GroupScan* p) {
 // Exclusive in-group prefixes E_b are carried across tiles, and so are the exclusive running extrema of
 // z = fl(E_b + in-block prefix) (any fixed association works: k_resample evaluates every c_i and every
 // block-start running max from these same stored E_b).  Returns the group partial.
+// W4 (k_group after the streaming pass): `part` holds kWaves wave partials per block (BlockPart fields: wave
+// total, max / min in-wave prefix, max / argmax, min / argmin), combined here into the block partial with
+// publish_iteration's association (((0 + t0) + t1) + ..., the running extrema of pre + prefix, waves in order).
+template <bool W4 = false>
 __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, const BlockPart* __restrict__ part,
                                                      BlockScan* __restrict__ bscan, GroupPart* __restrict__ gpart) {
   const int lane = lane_id();
@@ -1801,7 +1844,28 @@ __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, c
     const int b = b0 + t + lane;
     const bool vb = t + lane < nb;
     double sum = 0.0, maxrel = -INFINITY, minrel = INFINITY;
-    if (vb) {
+    if (vb && W4) {  // written by the previous launch: plain loads
+      const BlockPart* p = part + (size_t)b * kWaves;
+      BlockPart w[kWaves];
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) w[ww] = p[ww];
+      double pre = 0.0, bmx = w[0].maxw, bmn = w[0].minw;
+      int bix = w[0].argmax, bin = w[0].argmin;
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        const double a = pre + w[ww].maxrel, c = pre + w[ww].minrel;
+        maxrel = a > maxrel ? a : maxrel;
+        minrel = c < minrel ? c : minrel;
+        if (ww) {
+          cmb_max(bmx, bix, w[ww].maxw, w[ww].argmax);
+          cmb_min(bmn, bin, w[ww].minw, w[ww].argmin);
+        }
+        pre = pre + w[ww].sum;
+      }
+      sum = pre;
+      cmb_max(maxw, amax, bmx, bix);
+      cmb_min(minw, amin, bmn, bin);
+    } else if (vb) {
       const BlockPart* p = part + b;
       sum = ld_wt_d(&p->sum);
       maxrel = ld_wt_d(&p->maxrel);
@@ -2263,7 +2327,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
                                                          SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
-  __shared__ WeighLds sh;
   if (ctrl->done) return;  // the exit rule already fired (uniform)
   const int slot = ctrl->cur_slot;
   T* wout = slot ? w1 : w0;
@@ -2277,7 +2340,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   RawState<SP> R{};
   {
     const int n = vb * kBlock + (int)threadIdx.x;
-    load_state_prefetch<SP>(prior, fa.ld, n, n < fa.N && n >= 2, R);
+    load_state_prefetch<SP>(prior, fa.ld, in_planes(n, fa.N), n < fa.N && n >= 2, R);
   }
   stage_consts(fa, sc);
   __syncthreads();  // table + constants visible
@@ -2289,7 +2352,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     T A[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) A[q] = state_from_raw<T, SP>(R, q, fa.anc_in[q]);
-    load_state_prefetch<SP>(prior, fa.ld, n + step, n + step < fa.N && n + step >= 2, R);  // next block's particle
+    load_state_prefetch<SP>(prior, fa.ld, in_planes(n + step, fa.N), n + step < fa.N && n + step >= 2, R);  // next block
     T w = (T)0, P[12];
     if (valid) w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
     if (valid) {
@@ -2300,42 +2363,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     T mx, mn;
     int ix, in_;
     wave_weight_partials(w, valid, n, wi, rmx, rmn, mx, ix, mn, in_);
-    if (lane == 63) sh.tot[wv] = wi;
+    // the wave's partial, as it is (k_group combines a block's kWaves wave partials with publish_iteration's
+    // association): no LDS round trip, no block barrier and no serial combine in the loop
+    const double tot = lane_value(wi, 63);
     if (lane == 0) {
-      sh.rmax[wv] = rmx;
-      sh.rmin[wv] = rmn;
-      sh.mx[wv] = (double)mx;
-      sh.mn[wv] = (double)mn;
-      sh.ix[wv] = ix;
-      sh.in_[wv] = in_;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // publish_iteration's block partial, same association
-      double pre = 0.0, maxrel = -INFINITY, minrel = INFINITY, bmx = sh.mx[0], bmn = sh.mn[0];
-      int bix = sh.ix[0], bin = sh.in_[0];
-#pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) {
-        const double a = pre + sh.rmax[ww], b = pre + sh.rmin[ww];
-        maxrel = a > maxrel ? a : maxrel;
-        minrel = b < minrel ? b : minrel;
-        if (ww) {
-          cmb_max(bmx, bix, sh.mx[ww], sh.ix[ww]);
-          cmb_min(bmn, bin, sh.mn[ww], sh.in_[ww]);
-        }
-        pre = pre + sh.tot[ww];
-      }
       BlockPart q;
-      q.sum = pre;
-      q.maxrel = maxrel;
-      q.minrel = minrel;
-      q.maxw = bmx;
-      q.minw = bmn;
-      q.argmax = bix;
-      q.argmin = bin;
-      parts[vb] = q;
+      q.sum = tot;
+      q.maxrel = rmx;
+      q.minrel = rmn;
+      q.maxw = (double)mx;
+      q.minw = (double)mn;
+      q.argmax = ix;
+      q.argmin = in_;
+      parts[(size_t)vb * kWaves + wv] = q;
     }
-    __syncthreads();  // sh is reused by the next block (one barrier per block with double-buffered partials
-                      // measured 2-4 us slower at C4, profiles/r03/ab_r03b.log)
   }
 }
 
@@ -2352,8 +2393,8 @@ __global__ __launch_bounds__(64) void k_group(const FrameArgsT<T> fa, BlockPart*
                                               GroupPart* __restrict__ gpart1, const Ctrl* __restrict__ ctrl) {
   if (ctrl->done) return;
   const int slot = ctrl->cur_slot;
-  (void)propagate_group(fa.nblk, fa.gsz, (int)blockIdx.x, slot ? part1 : part0, slot ? bscan1 : bscan0,
-                        slot ? gpart1 : gpart0);
+  (void)propagate_group<true>(fa.nblk, fa.gsz, (int)blockIdx.x, slot ? part1 : part0, slot ? bscan1 : bscan0,
+                              slot ? gpart1 : gpart0);
 }
 template <typename T, int RNG>
 __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
@@ -3237,21 +3278,20 @@ __device__ __forceinline__ void resample_block(
   // k_resample_final writes the record
   if (!c.done || !c.accepted) return;
   // the kept iteration's stored propagated set, gathered as raw state values (no regeneration).  fp16: planes
-  // 2j and 2j + 1 land in the two halves of word j (buffer_load_short_d16 / _d16_hi), which is the row layout
-  // resample_phase stages, so the words need no packing instruction
+  // 2j and 2j + 1 are word j (one dword of the pair plane), which is the row layout resample_phase stages
   RawState<SP> KR{};
   if (kept) {
     const SP* src = c.kept_slot ? prop1 : prop0;
-    // buffer-resource planes: every lane loads (a lane past N reads inside the planes or gets 0 from the
-    // resource bound), so no branch: behind one, the weights' wait before the block scan became vmcnt(0) and
-    // also waited for these loads
+    // buffer-resource planes: every lane loads (a lane past N at the index clamped into [0, N), in_planes), so
+    // no branch: behind one, the weights' wait before the block scan became vmcnt(0) and also waited for these
+    // loads
     if constexpr (std::is_same<SP, __half>::value) {
-      load_state_prefetch<SP>(src, fa.ld, n, true, KR);
+      load_state_prefetch<SP>(src, fa.ld, in_planes(n, fa.N), true, KR);
     } else {
       SP V[12];
 #pragma unroll
       for (int q = 0; q < 12; ++q) V[q] = SP(0.0f);
-      if (BufPlanes<SP>::value || valid) load_state_raw<SP>(src, fa.ld, n, V);
+      if (BufPlanes<SP>::value || valid) load_state_raw<SP>(src, fa.ld, in_planes(n, fa.N), V);
 #pragma unroll
       for (int q = 0; q < 12; ++q) A[q] = V[q];
     }

@@ -217,7 +217,8 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   for (int i = 0; i < 2; ++i) {
     ok &= hipMalloc(&c->d_state[i], state_bytes) == hipSuccess;
     ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->ws) == hipSuccess;
-    ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * sizeof(BlockPart)) == hipSuccess;
+    // kWaves entries per block: the streaming weighing pass stores wave partials (k_group combines them)
+    ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * kWaves * sizeof(BlockPart)) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_bscan[i], (size_t)c->max_blk * sizeof(BlockScan)) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_gpart[i], (size_t)c->max_grp * sizeof(GroupPart)) == hipSuccess;
   }
