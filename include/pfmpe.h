@@ -42,7 +42,8 @@ enum {
 
 /* particle state storage in HBM (SoA planes).  F16: fp16 deltas to an anchor pose per particle set
  * (the frame's current pose for a resampled set, the first particle for pfmpe_set_prior), fp32 compute
- * and fp32 weights: 24 B per particle (BASELINE.json configs[3]). */
+ * and fp32 weights: 24 B per particle (BASELINE.json configs[3]), stored as 6 planes of fp16 pairs.  The
+ * layout is internal: every entry point exchanges poses as 12 doubles per particle. */
 enum { PFMPE_STATE_F32 = 0, PFMPE_STATE_F64 = 1, PFMPE_STATE_F16 = 2 };
 
 /* motion / resample random streams */

@@ -26,6 +26,7 @@ pmc() {  # pmc <name> <bench args> -- counters per pass as separate runs
   done
   python3 scripts/pmc_summary.py gpurun_out/${t}_pmc_$name --json gpurun_out/${t}_pmc_$name.json > gpurun_out/${t}_pmc_$name.txt 2>&1
 }
+if [ "${PHASE:-A}" = A ]; then
 run bench_c2 400 python -u bench.py
 run bench_c2_driver 400 python -u bench.py --steps 20 --warmup 5 --cpu-frames 0  # the driver's flags
 run bench_c3 200 python -u bench.py --config C3 --cpu-frames 0 --steps 50 --warmup 5 --multi-sweep 1,4
@@ -36,9 +37,11 @@ run prof_c4 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${t}_prof_c4 -o r
 run prof_c5 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${t}_prof_c5 -o run --output-format csv -- python3 bench.py --config C5 --cpu-frames 0 --no-timing --worst-frames 0 --steps 50 --warmup 5
 run prof_multi16 200 rocprofv3 --kernel-trace --stats -d gpurun_out/${t}_prof_multi16 -o run --output-format csv -- python3 bench.py --cpu-frames 0 --no-timing --worst-frames 0 --steps 10 --warmup 2 --multi-sweep 16 --multi-steps 100
 for p in c2 c4 c5 multi16; do python3 scripts/trace_summary.py gpurun_out/${t}_prof_$p 12 > gpurun_out/${t}_prof_${p}_summary.txt 2>&1; done
-pmc c2 "--steps 50 --warmup 5 --multi-steps 5"
-pmc c4 "--config C4 --steps 20 --warmup 3"
-pmc c5 "--config C5 --steps 20 --warmup 3"
-pmc multi16 "--steps 5 --warmup 2 --multi-sweep 16 --multi-steps 60"
+fi
+if [ "${PHASE:-A}" = B ]; then
+pmc c2 "--steps 50 --warmup 5 --multi-sweep none --exact-steps 0 --scale-ref-steps 0"
+pmc c4 "--config C4 --steps 20 --warmup 3 --multi-sweep none"
+pmc c5 "--config C5 --steps 20 --warmup 3 --multi-sweep none"
 run init 200 python -u scripts/bench_init.py
 echo "== done $(date +%T)"
+fi
