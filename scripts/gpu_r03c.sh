@@ -5,4 +5,4 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
 bash scripts/gpu_suite.sh || exit 1
 timeout -k 10 120 ./scripts/micro/copy_roof > gpurun_out/copy_roof.log 2>&1 || { cat gpurun_out/copy_roof.log; exit 1; }
 cat gpurun_out/copy_roof.log
-AB_CONFIGS="C4 C5 C2" bash scripts/ab_r03.sh > gpurun_out/ab_r03c.log 2>&1; rc=$?; cat gpurun_out/ab_r03c.log; exit $rc
+AB_CONFIGS="${AB_CONFIGS:-C4 C5 C2}" bash scripts/ab_r03.sh > gpurun_out/ab_r03c.log 2>&1; rc=$?; cat gpurun_out/ab_r03c.log; exit $rc
