@@ -375,10 +375,11 @@ struct Seq {
     SP* prop1 = c->keep_prop ? (SP*)c->d_prop[1] : nullptr;
     // The streaming weighing pass (k_weigh_stream: resident blocks looping over the 256-particle blocks, the
     // next particle's state prefetched) with the group / top hand-off as two small launches.  It wins for
-    // <= 8 markers (C5: 52 -> 31 us weighing, 104 -> 95 us per frame; C4 with the 6-wave fp16 build: weighing
-    // 265 -> 233 us, of which the 611-group hand-off takes back ~21 us).  At 12 markers (C3) the weighing is
-    // VALU bound and the extra launches cost more than the prefetch saves.
-    const bool stream = !(c->diag & kDiagNoStream) && ((c->diag & kDiagForceStream) || MAXM <= 8);
+    // every marker bucket: C5 52 -> 31 us weighing (round 2), C4 265 -> 233 us; at 12 markers (C3) it lost while
+    // the pass staged block partials through LDS behind two barriers per block, and wins since it stores wave
+    // partials (round 3: C3 116-117 -> 111-113 us per frame, profiles/r03/ab_c3_stream.log).
+    // kDiagNoStream / kDiagForceStream pick either pass for tests and A/B.
+    const bool stream = !(c->diag & kDiagNoStream);
     c->last_weigh_pass = stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS;
     if (stream) {
       const void* fn = c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
