@@ -2396,6 +2396,25 @@ __global__ __launch_bounds__(64) void k_group(const FrameArgsT<T> fa, BlockPart*
   (void)propagate_group<true>(fa.nblk, fa.gsz, (int)blockIdx.x, slot ? part1 : part0, slot ? bscan1 : bscan0,
                               slot ? gpart1 : gpart0);
 }
+// k_group and k_top as ONE launch when the groups fit one tile (<= 64: C3, C5): every block scans its group, and
+// the last to arrive on the top counter (write-through group partials, drained before the arrival, exactly the
+// one-block pass's publish_iteration tail) runs propagate_top.  Saves the second launch and its gap; > 64 groups
+// keep k_group + k_top_wide (a one-wave serial top over many tiles is slower than the wide one).
+template <typename T, int RNG>
+__global__ __launch_bounds__(64) void k_group_top(const FrameArgsT<T> fa, BlockPart* __restrict__ part0,
+                                                  BlockPart* __restrict__ part1, BlockScan* __restrict__ bscan0,
+                                                  BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+                                                  GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                                  Ctrl* __restrict__ ctrl, uint32_t* __restrict__ tcount, int iter) {
+  if (ctrl->done) return;  // every block reads ctrl before it arrives, so before the top can rewrite it
+  const int slot = ctrl->cur_slot;
+  const GroupPart gr = propagate_group<true>(fa.nblk, fa.gsz, (int)blockIdx.x, slot ? part1 : part0,
+                                             slot ? bscan1 : bscan0, slot ? gpart1 : gpart0);
+  const bool single = fa.ngrp == 1;
+  if (!single && !wave_arrive_last(tcount, fa.ngrp)) return;
+  propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, nullptr, 0u, gr, single, slot);
+}
+
 template <typename T, int RNG>
 __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
                                             GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,

@@ -405,6 +405,11 @@ struct Seq {
       // the top's group partials fit LDS up to 1,365 groups (22M particles); beyond, it reads them from L2
       const size_t glds = fa.ngrp > 64 ? (size_t)fa.ngrp * sizeof(GroupPart) : 0;
       const bool staged = glds > 0 && glds <= 64 * 1024;
+      if (fa.ngrp <= 64 && !(c->diag & kDiagSerialTop))  // one tile: group scans + top in one launch
+        return launch_ext(c, PFMPE_K_AUX, [&] {
+          klaunch(c, k_group_top<T, RNG>, dim3(fa.ngrp), dim3(64), 0, fa, c->d_part[0], c->d_part[1], c->d_bscan[0],
+                  c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, tcount, iter);
+        });
       return launch_ext(c, PFMPE_K_AUX, [&] {
         klaunch(c, k_group<T>, dim3(fa.ngrp), dim3(64), 0, fa, c->d_part[0], c->d_part[1],
                            c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], (const Ctrl*)c->d_ctrl);
