@@ -41,9 +41,9 @@ STREAMS = [
 ]
 
 
-def _streams(n_frames):
+def _streams(n_frames, cfgs=STREAMS):
     out = []
-    for s, (N, M, B, heavy, how) in enumerate(STREAMS):
+    for s, (N, M, B, heavy, how) in enumerate(cfgs):
         cfg = syn.StreamConfig(f"s{s}", M=M, B=B, N=N, heavy=heavy, seed=s)
         st = syn.make_stream(cfg, n_frames, t0=0.5 + 0.1 * s)
         frames = []
@@ -88,13 +88,10 @@ def _same(a, b, tag):
             assert np.array_equal(a[k], b[k]), (tag, k)
 
 
-@pytest.mark.parametrize("state,rng", [(pf.STATE_F64, pf.RNG_REFERENCE), (pf.STATE_F32, pf.RNG_PHILOX),
-                                       (pf.STATE_F16, pf.RNG_PHILOX)])
-def test_multi_equals_single_streams(state, rng):
-    n_frames = 3
-    streams = _streams(n_frames)
+def _check_batch(state, rng, n_frames, cfgs=STREAMS):
+    streams = _streams(n_frames, cfgs)
     batch, solo = [], []
-    for (st, frames, how), (N, M, *_rest) in zip(streams, STREAMS):
+    for (st, frames, how), (N, M, *_rest) in zip(streams, cfgs):
         pair = []
         for fused in (2, 0):  # the solo engine takes its default shape; the batch always runs two launches
             eng = _engine(N, M, state, rng, fused=fused)
@@ -122,6 +119,21 @@ def test_multi_equals_single_streams(state, rng):
     finally:
         for e in batch + solo:
             e.close()
+
+
+@pytest.mark.parametrize("state,rng", [(pf.STATE_F64, pf.RNG_REFERENCE), (pf.STATE_F32, pf.RNG_PHILOX),
+                                       (pf.STATE_F16, pf.RNG_PHILOX)])
+def test_multi_equals_single_streams(state, rng):
+    _check_batch(state, rng, 3)
+
+
+def test_multi_restaging_after_later_rounds():
+    """Every frame's later iteration rounds (the occluded stream) stage a one-stream layout into the batch's
+    host image; the next frame's first round stages the full layout at the same addresses.  The staging launch
+    must read the image the host just wrote, never a cached copy of the previous round's."""
+    cfgs = [(4099, 5, 50, False, "occlude"), (300, 5, 3, False, ""), (1000, 5, 20, False, ""),
+            (2048, 12, 200, True, "")]
+    _check_batch(pf.STATE_F64, pf.RNG_REFERENCE, 8, cfgs)
 
 
 def test_multi_fp64_stream_matches_oracle():
