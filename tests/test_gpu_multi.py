@@ -88,9 +88,9 @@ def _same(a, b, tag):
             assert np.array_equal(a[k], b[k]), (tag, k)
 
 
-def _check_batch(state, rng, n_frames, cfgs=STREAMS):
+def _check_batch(state, rng, n_frames, cfgs=STREAMS, strict_occlude=True):
     streams = _streams(n_frames, cfgs)
-    batch, solo = [], []
+    batch, solo, occl_iters = [], [], []
     for (st, frames, how), (N, M, *_rest) in zip(streams, cfgs):
         pair = []
         for fused in (2, 0):  # the solo engine takes its default shape; the batch always runs two launches
@@ -112,13 +112,15 @@ def _check_batch(state, rng, n_frames, cfgs=STREAMS):
                 ref_out = solo[s].step(_frame(solo[s], fr, blobs, how, seeds[s], f))
                 _same(_snapshot(batch[s], outs[s]), _snapshot(solo[s], ref_out), (state, s, f))
                 if how == "occlude":
-                    assert outs[s].iters == 80
+                    occl_iters.append(outs[s].iters)
+                    assert outs[s].iters == 80 or not strict_occlude
                 if how == "empty":
                     assert outs[s].flag_fail == pf.FLAG_REINIT
             assert batch[0].info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
     finally:
         for e in batch + solo:
             e.close()
+    return occl_iters
 
 
 @pytest.mark.parametrize("state,rng", [(pf.STATE_F64, pf.RNG_REFERENCE), (pf.STATE_F32, pf.RNG_PHILOX),
@@ -133,7 +135,8 @@ def test_multi_restaging_after_later_rounds():
     must read the image the host just wrote, never a cached copy of the previous round's."""
     cfgs = [(4099, 5, 50, False, "occlude"), (300, 5, 3, False, ""), (1000, 5, 20, False, ""),
             (2048, 12, 200, True, "")]
-    _check_batch(pf.STATE_F64, pf.RNG_REFERENCE, 8, cfgs)
+    iters = _check_batch(pf.STATE_F64, pf.RNG_REFERENCE, 8, cfgs, strict_occlude=False)
+    assert sum(i > 1 for i in iters[:-1]) >= 2, iters  # frames with later rounds, each followed by another frame
 
 
 def test_multi_fp64_stream_matches_oracle():
