@@ -2715,22 +2715,20 @@ template <typename T, typename SP>
 __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __restrict__ host,
                                                         unsigned char* __restrict__ dev, uint32_t doff, uint32_t tbytes,
                                                         uint32_t boff) {
-  typedef __attribute__((address_space(1))) const u32x4_t gv4_t;
   // The host rewrote the image with plain CPU stores that the runtime does not see, and the dispatch's own
-  // acquire is agent scope: a system-scope acquire first, so that no line an earlier batch or round read from
-  // the image (same addresses, other contents: a later round stages a smaller layout) is served from a cache.
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  // acquire is agent scope, which leaves cached copies of host memory valid: a line an earlier batch or round
+  // read from the image (same addresses, other contents: a later round stages a smaller layout) could be
+  // served stale.  So every read of the image is a system-scope atomic load (a vector load with sc0 sc1,
+  // coherent with the host; never a scalar load), which needs no cache invalidate in front of it.
+  auto host_ld = [](const auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
   const int s = blockIdx.x;
   const StreamDesc<T, SP>* hd = (const StreamDesc<T, SP>*)(host + doff) + s;
   static_assert(sizeof(StreamDesc<T, SP>) % 16 == 0, "descriptor as 16-B words");
   {
-    gv4_t* src = (gv4_t*)hd;
-    u32x4_t* dst = (u32x4_t*)((StreamDesc<T, SP>*)(dev + doff) + s);
-    for (int i = threadIdx.x; i < (int)(sizeof(StreamDesc<T, SP>) / 16); i += kBlock) dst[i] = src[i];
+    const uint64_t* src = (const uint64_t*)hd;
+    uint64_t* dst = (uint64_t*)((StreamDesc<T, SP>*)(dev + doff) + s);
+    for (int i = threadIdx.x; i < (int)(sizeof(StreamDesc<T, SP>) / 8); i += kBlock) dst[i] = host_ld(src + i);
   }
-  // the image's uniform fields as system-scope vector loads: a scalar load would go through the scalar cache
-  // path, which the fence's vector-cache invalidate does not order
-  auto host_ld = [](const auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
   const int first = __builtin_amdgcn_readfirstlane(host_ld(&hd->first_blk));
   const int nblk = __builtin_amdgcn_readfirstlane(host_ld(&hd->fa.nblk));
   const unsigned char* tab = (const unsigned char*)host_ld((const uintptr_t*)&hd->table);
@@ -2738,10 +2736,10 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
   const uintptr_t to = (uintptr_t)tab - (uintptr_t)dev;  // wraps above tbytes for bank tables
   if (to < tbytes) {
-    gv4_t* src = (gv4_t*)(host + to);
-    u32x4_t* dst = (u32x4_t*)(dev + to);
-    const int n4 = __builtin_amdgcn_readfirstlane(host_ld(&hd->fa.tbytes)) / 16;
-    for (int i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
+    const uint64_t* src = (const uint64_t*)(host + to);
+    uint64_t* dst = (uint64_t*)(dev + to);
+    const int n8 = __builtin_amdgcn_readfirstlane(host_ld(&hd->fa.tbytes)) / 8;
+    for (int i = threadIdx.x; i < n8; i += kBlock) dst[i] = host_ld(src + i);
   }
 }
 
