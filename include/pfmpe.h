@@ -345,8 +345,9 @@ enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 aft
        PFMPE_INFO_LAST_WEIGH_PASS = 6 };/* PFMPE_WEIGH_* of the last two-launch weighing (-1: none)  */
 /* The two-launch shape's weighing pass: one block per 256 particles (k_propagate_weigh), or
  * resident blocks streaming over them with the next block's state prefetched (k_weigh_stream + k_group +
- * k_top; chosen for <= 8 markers).  Both give bit-identical results. */
-enum { PFMPE_WEIGH_BLOCKS = 0, PFMPE_WEIGH_STREAM = 1 };
+ * k_top), or the streaming pass with two particles per lane in packed fp32 (k_weigh_pk: 5 markers, fp32 / fp16
+ * state, the Philox stream, the blob grid).  All give bit-identical results. */
+enum { PFMPE_WEIGH_BLOCKS = 0, PFMPE_WEIGH_STREAM = 1, PFMPE_WEIGH_PK = 2 };
 int pfmpe_get_info(const pfmpe_ctx* ctx, int key, int64_t* value);
 
 /* ----------------------------------------------------------------------- device-resident inputs */

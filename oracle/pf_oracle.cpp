@@ -261,6 +261,10 @@ typedef struct {
   int exit_cap;      // 5  (PE:616  M*min(5,numLED))
   int accept_cap;    // 3  (PE:633  M*min(3,numLED))
   int rng_mode;      // 0 reference (minstd_rand0 + generate_canonical), 1 Philox4x32-10
+  int fast_search;   // test speed only: 1 = the cumulative search of PE:674-679 by binary search over the
+                     // running max of the SAME sequential cumulative sums (first i with c_i >= r equals the
+                     // first i with max(c_0..c_i) >= r), identical counts/indices; 0 = the reference's O(N^2)
+                     // scan (the cpu_baseline timing keeps 0)
 } orc_params;
 
 typedef struct {
@@ -495,6 +499,16 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
     out->accepted = 1;
     out->flag_fail = 1;
     // PE:637 inner branch is unreachable (2/3*numLED == 0); uncertainty = 1; resample (PE:666)
+    std::vector<double> runmax;  // fast_search: running max of the scan's own sequential sums
+    if (prm->fast_search) {
+      runmax.resize(N);
+      double c = 0, r = -INFINITY;
+      for (int i = 0; i < N; ++i) {
+        c += probPart[i];
+        r = c > r ? c : r;
+        runmax[i] = r;
+      }
+    }
     for (int numResamples = 0; numResamples < N_Resamples; numResamples++) {
       double u;
       if (prm->rng_mode == RNG_REFERENCE) {
@@ -506,13 +520,21 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
         u = u53(o[0], o[1]);
       }
       const double randVar = (numResamples + u) / N_Resamples;
-      probPartSum = 0;
-      for (int idxParticle = 0; idxParticle < N; idxParticle++) {
-        probPartSum += probPart[idxParticle];
-        if (probPartSum >= randVar) {
-          Particle_index = idxParticle;
-          counterMeas[idxParticle]++;
-          break;
+      if (prm->fast_search) {
+        const auto it = std::lower_bound(runmax.begin(), runmax.end(), randVar);  // first runmax_i >= randVar
+        if (it != runmax.end()) {
+          Particle_index = (int)(it - runmax.begin());
+          counterMeas[Particle_index]++;
+        }
+      } else {
+        probPartSum = 0;
+        for (int idxParticle = 0; idxParticle < N; idxParticle++) {
+          probPartSum += probPart[idxParticle];
+          if (probPartSum >= randVar) {
+            Particle_index = idxParticle;
+            counterMeas[idxParticle]++;
+            break;
+          }
         }
       }
       if (resample_idx_out) resample_idx_out[numResamples] = Particle_index;

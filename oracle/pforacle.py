@@ -24,6 +24,7 @@ class OrcParams(C.Structure):
         ("trans_min", C.c_double), ("trans_max", C.c_double),
         ("growth", C.c_double),
         ("max_iter", C.c_int), ("exit_cap", C.c_int), ("accept_cap", C.c_int), ("rng_mode", C.c_int),
+        ("fast_search", C.c_int),
     ]
 
 
@@ -200,9 +201,11 @@ def uniform_draws(seed, a, b, n):
 
 
 def make_params(tol=5.0, tol_pf=4.0, ang=(-0.015, 0.015), trans=(-0.035, 0.035), growth=0.025,
-                max_iter=80, exit_cap=5, accept_cap=3, rng_mode=RNG_PHILOX) -> OrcParams:
+                max_iter=80, exit_cap=5, accept_cap=3, rng_mode=RNG_PHILOX, fast_search=0) -> OrcParams:
+    """fast_search=1: the resampler's cumulative search by binary search (identical results, O(N log N);
+    for long closed-loop tests at 100k particles).  0 keeps the reference's O(N^2) scan (cpu_baseline)."""
     return OrcParams(tol, tol_pf, ang[0], ang[1], trans[0], trans[1], growth, max_iter, exit_cap, accept_cap,
-                     rng_mode)
+                     rng_mode, fast_search)
 
 
 def pf_step(markers, K, params: OrcParams, prior, current_pose, predicted_pose, prediction, blobs,

@@ -44,6 +44,7 @@
 #include <hip/hip_fp16.h>
 
 #include "pf_rng.hpp"
+#include "pf_desc_tag.hpp"
 
 namespace pfmpe {
 
@@ -1488,7 +1489,10 @@ enum : int {
   kDiagSortedScore = 256, // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
   kDiagNoStream = 512,     // two-launch path: never the streaming weighing pass (k_weigh_stream + k_group + k_top)
   kDiagForceStream = 1024, // two-launch path: always the streaming weighing pass (tests / A/B)
-  kDiagSerialTop = 2048    // streaming pass with > 64 groups: the one-wave k_top instead of k_top_wide (A/B)
+  kDiagSerialTop = 2048,   // streaming pass with > 64 groups: the one-wave k_top instead of k_top_wide (A/B)
+  kDiagNoPk = 4096,        // two-launch path: never the two-particles-per-lane pass k_weigh_pk (A/B, tests)
+  kDiagCorruptDesc = 8192  // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
+                           // staging check; the altered word is a key word, never a pointer)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -1690,6 +1694,16 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
   ncx = std::max(1, ncx);
   ncy = std::max(1, ncy);
   const float inv_c = (float)(1.0 / cs), gx0f = (float)gx0, gy0f = (float)gy0;
+  // The device's cell coordinate fma(u, inv_c, ox) rounds twice (ox = fl(-gx0 * inv_c), then the fma), each by at
+  // most half an ulp of a value below |ox| + ncx cells, i.e. 2^-24 (|ox| + ncx) cells of cs px.  The lists hold
+  // every blob within m = tolq + 0.01 px of a cell, so the proof needs that error well inside m - tolq = 0.01 px:
+  // far-out blob coordinates (|gx0| ~ 1e5 px and beyond) make |ox| large, and then the x-buckets
+  // serve instead of the grid.
+  {
+    const double ex = std::ldexp(std::abs((double)gx0f) * (double)inv_c + ncx + 1.0, -23) * cs;
+    const double ey = std::ldexp(std::abs((double)gy0f) * (double)inv_c + ncy + 1.0, -23) * cs;
+    if (!(std::max(ex, ey) <= 0.25 * (m - tolq))) return total;
+  }
   auto crange = [&](double lo, double hi, float inv, float org, int n, int& c0, int& c1) {
     const double f0 = (lo - (double)org) * (double)inv, f1 = (hi - (double)org) * (double)inv;
     c0 = (int)std::max(0.0, std::min((double)(n - 1), std::floor(f0)));
@@ -2704,6 +2718,8 @@ struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B wor
   RecOut* out;
   int32_t seq;
   int32_t first_blk;  // the stream's first block in the grid
+  uint64_t gen;       // the batch generation (staging launch counter; every kernel of the round gets it)
+  uint64_t tag;       // desc_tag over every word before this one (pf_desc_tag.hpp)
 };
 
 // Batch staging (block s = stream s): the stream's descriptor and, for host-supplied blobs, its table, from
@@ -2711,46 +2727,77 @@ struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B wor
 // A launch in the batch's own stream instead of a host-to-device copy: no copy-engine hand-off in front of
 // the weighing launch.  dev / host: the device scratch and its pinned host image (same layout); a table
 // pointer inside [dev, dev + tbytes) is a staged host table.
+// The descriptor is checked before any of its words is used (pf_desc_tag.hpp): the tag recomputed over the words
+// this block read must equal the tag word, and the generation word must equal `gen`.  status[s] = gen then; a
+// failed check leaves status[s] != gen, writes no map entry and stages no table, and every later kernel of the
+// round skips the stream (batch_block / k_resample_final_multi test status[s] == gen), so no pointer of a bad
+// descriptor is ever followed.  The host finds the missing frame record and reports the descriptor the device
+// saw (its HBM copy, written here word for word) against the one it wrote.
 template <typename T, typename SP>
 __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __restrict__ host,
                                                         unsigned char* __restrict__ dev, uint32_t doff, uint32_t tbytes,
-                                                        uint32_t boff) {
+                                                        uint32_t boff, uint32_t* __restrict__ status, uint32_t gen) {
   // The host rewrote the image with plain CPU stores that the runtime does not see, and the dispatch's own
   // acquire is agent scope, which leaves cached copies of host memory valid: a line an earlier batch or round
   // read from the image (same addresses, other contents: a later round stages a smaller layout) could be
   // served stale.  So every read of the image is a system-scope atomic load (a vector load with sc0 sc1,
   // coherent with the host; never a scalar load), which needs no cache invalidate in front of it.
   auto host_ld = [](const auto* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+  using Desc = StreamDesc<T, SP>;
   const int s = blockIdx.x;
-  const StreamDesc<T, SP>* hd = (const StreamDesc<T, SP>*)(host + doff) + s;
-  static_assert(sizeof(StreamDesc<T, SP>) % 16 == 0, "descriptor as 16-B words");
+  const Desc* hd = (const Desc*)(host + doff) + s;
+  static_assert(sizeof(Desc) % 16 == 0, "descriptor as 16-B words");
+  constexpr int kWords = (int)(sizeof(Desc) / 8), kTagWords = (int)(offsetof(Desc, tag) / 8);
+  static_assert(offsetof(Desc, tag) % 8 == 0 && offsetof(Desc, gen) + 8 == offsetof(Desc, tag), "tag layout");
+  __shared__ unsigned long long h;
+  __shared__ Desc ld;  // the words as this block read them (each word is read by one thread: no global re-read)
+  if (threadIdx.x == 0) h = 0ull;
+  __syncthreads();
   {
     const uint64_t* src = (const uint64_t*)hd;
-    uint64_t* dst = (uint64_t*)((StreamDesc<T, SP>*)(dev + doff) + s);
-    for (int i = threadIdx.x; i < (int)(sizeof(StreamDesc<T, SP>) / 8); i += kBlock) dst[i] = host_ld(src + i);
+    uint64_t* dst = (uint64_t*)((Desc*)(dev + doff) + s);
+    uint64_t mine = 0;
+    for (int i = threadIdx.x; i < kWords; i += kBlock) {
+      const uint64_t v = host_ld(src + i);
+      dst[i] = v;
+      ((uint64_t*)&ld)[i] = v;
+      if (i < kTagWords) mine ^= tag_mix(v, (uint32_t)i);
+    }
+    if (mine) atomicXor(&h, (unsigned long long)mine);
   }
-  const int first = __builtin_amdgcn_readfirstlane(host_ld(&hd->first_blk));
-  const int nblk = __builtin_amdgcn_readfirstlane(host_ld(&hd->fa.nblk));
-  const unsigned char* tab = (const unsigned char*)host_ld((const uintptr_t*)&hd->table);
+  __syncthreads();  // the block's words and the tag terms in LDS
+  const bool ok = __builtin_amdgcn_readfirstlane((int)(h == (unsigned long long)ld.tag && ld.gen == (uint64_t)gen));
+  if (!ok) {
+    if (threadIdx.x == 0) status[s] = ~gen;
+    return;
+  }
+  const int first = __builtin_amdgcn_readfirstlane(ld.first_blk);
+  const int nblk = __builtin_amdgcn_readfirstlane(ld.fa.nblk);
+  const unsigned char* tab = ld.table;
   uint16_t* bm = (uint16_t*)(dev + boff);
   for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
   const uintptr_t to = (uintptr_t)tab - (uintptr_t)dev;  // wraps above tbytes for bank tables
   if (to < tbytes) {
     const uint64_t* src = (const uint64_t*)(host + to);
     uint64_t* dst = (uint64_t*)(dev + to);
-    const int n8 = __builtin_amdgcn_readfirstlane(host_ld(&hd->fa.tbytes)) / 8;
+    const int n8 = __builtin_amdgcn_readfirstlane(ld.fa.tbytes) / 8;
     for (int i = threadIdx.x; i < n8; i += kBlock) dst[i] = host_ld(src + i);
   }
+  if (threadIdx.x == 0) status[s] = gen;
 }
 
 // The block's stream and its stream-local block index, or -1 for a block the map does not place inside a
-// stream of this batch (never on a consistent batch: the host audits the layout before every launch,
-// pfmpe_ctx.hpp audit_batch; the guard keeps a corrupt map from turning into out-of-range accesses).
+// stream of this batch whose descriptor passed the staging check (never on a consistent batch: the host audits
+// the layout before every launch, pfmpe_ctx.hpp audit_batch, and tags every descriptor; the guard keeps a
+// corrupt map or descriptor from turning into out-of-range accesses).  A stale map entry cannot misplace a
+// block: the range test runs against a checked descriptor, and checked streams' ranges are disjoint.
 template <typename T, typename SP>
 __device__ __forceinline__ int batch_block(const StreamDesc<T, SP>* __restrict__ descs,
-                                           const uint16_t* __restrict__ bmap, int S, int* s_out) {
+                                           const uint16_t* __restrict__ bmap, int S, const uint32_t* __restrict__ status,
+                                           uint32_t gen, int* s_out) {
   const int s = __builtin_amdgcn_readfirstlane((int)bmap[blockIdx.x]);
   if (s >= S) return -1;
+  if (__builtin_amdgcn_readfirstlane(status[s]) != gen) return -1;
   const int blk = (int)blockIdx.x - __builtin_amdgcn_readfirstlane(descs[s].first_blk);
   if (blk < 0 || blk >= __builtin_amdgcn_readfirstlane(descs[s].fa.nblk)) return -1;
   *s_out = s;
@@ -2759,12 +2806,14 @@ __device__ __forceinline__ int batch_block(const StreamDesc<T, SP>* __restrict__
 
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) void k_propagate_weigh_multi(const StreamDesc<T, SP>* __restrict__ descs,
-                                                                  const uint16_t* __restrict__ bmap, int S, int iter) {
+                                                                  const uint16_t* __restrict__ bmap, int S,
+                                                                  const uint32_t* __restrict__ status, uint32_t gen,
+                                                                  int iter) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ LdsConst<T> sc;
   __shared__ WeighLds sh;
   int s = 0;
-  const int blk = batch_block(descs, bmap, S, &s);
+  const int blk = batch_block(descs, bmap, S, status, gen, &s);
   if (blk < 0) return;
   const StreamDesc<T, SP>& d = descs[s];
   propagate_weigh_block<T, RNG, MAXM, PRUNE, SP, true>(d.fa, (const uint32_t*)&d.fa, blk, d.table,
@@ -3362,12 +3411,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? P
 
 template <typename T, int RNG, int MAXM, typename SP, bool KEPT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? PFMPE_RESAMPLE_KEPT_MIN_WAVES : PFMPE_RESAMPLE_MIN_WAVES))) void k_resample_multi(
-    const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S) {
+    const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S,
+    const uint32_t* __restrict__ status, uint32_t gen) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
   int s = 0;
-  const int blk = batch_block(descs, bmap, S, &s);
+  const int blk = batch_block(descs, bmap, S, status, gen, &s);
   if (blk < 0) return;
   const StreamDesc<T, SP>& d = descs[s];
   resample_block<T, RNG, MAXM, SP, true, KEPT>(d.fa, (const uint32_t*)&d.fa, blk, d.ctrl, d.table,
@@ -3514,8 +3564,11 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
 }
 // batched: block s finishes stream s
 template <typename T, int RNG, int MAXM, typename SP>
-__global__ __launch_bounds__(kFinalBlock) void k_resample_final_multi(const StreamDesc<T, SP>* __restrict__ descs) {
+__global__ __launch_bounds__(kFinalBlock) void k_resample_final_multi(const StreamDesc<T, SP>* __restrict__ descs,
+                                                                        const uint32_t* __restrict__ status,
+                                                                        uint32_t gen) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (__builtin_amdgcn_readfirstlane(status[blockIdx.x]) != gen) return;  // descriptor failed the staging check
   const StreamDesc<T, SP>& d = descs[blockIdx.x];
   resample_final_block<T, RNG, MAXM, SP, true>(d.fa, (const uint32_t*)&d.fa, d.ctrl, d.table, d.prior, d.cpart, d.cand,
                                          d.mlpose, d.out, d.seq, nullptr, d.prop0 ? 1 : 0, smem);
@@ -4180,3 +4233,5 @@ __global__ void k_weights_export(const T* __restrict__ w, double* __restrict__ o
 }
 
 }  // namespace pfmpe
+
+#include "pf_weigh_pk.hpp"

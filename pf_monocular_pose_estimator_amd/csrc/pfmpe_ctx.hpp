@@ -117,6 +117,7 @@ struct pfmpe_ctx {
   unsigned char* h_multi = nullptr;
   unsigned char* hd_multi = nullptr;  // device address of h_multi
   size_t multi_cap = 0;
+  uint32_t multi_gen = 0;  // batch generation: one per staging launch this context leads (StreamDesc::gen)
   // Cross-stream ordering.  A context's work runs on its own stream (pfmpe_step, read-backs, ...) or, inside a
   // batch, on the batch leader's stream.  last_stream is where its latest work went (nullptr: none since
   // create); when the next work goes to a different stream it is ordered after that work: through the
@@ -349,19 +350,39 @@ inline int ensure_prop(pfmpe_ctx* c) {
 // tables [0, tbytes), then `na` stream descriptors from doff, then the uint16 block -> stream map of `total`
 // blocks from boff; `need` bytes in all.
 struct BatchLayout {
-  size_t doff, boff, need;
+  size_t doff, boff, soff, need;
 };
 template <typename Desc>
 inline BatchLayout batch_layout(int na, int64_t total, size_t tbytes) {
   BatchLayout L;
   L.doff = tbytes;
   L.boff = L.doff + ((size_t)na * sizeof(Desc) + 255) / 256 * 256;
-  L.need = L.boff + (size_t)total * sizeof(uint16_t) + 256;
+  L.soff = L.boff + ((size_t)total * sizeof(uint16_t) + 255) / 256 * 256;  // uint32 status[na] (k_stage_multi)
+  L.need = L.soff + (size_t)na * sizeof(uint32_t) + 256;
   return L;
 }
 // Blocks per batch accepted by pfmpe_step_multi (PFMPE_E_CAP above): the size the GPU tests cover
 // (tests/test_gpu_multi.py: 4 x 10M fp16 particles in one batch = 156,252 blocks; 32 x 1M in the bench).
 constexpr int64_t kMultiMaxBlocks = 160000;
+
+// The frames k_weigh_pk covers (pf_weigh_pk.hpp): fp32 compute, the Philox stream, exactly five markers (the
+// instance), fp32 or fp16 pair-plane state, and per frame: the blob grid on (which implies pruning and fp32), the
+// short sincos polynomials, an identity camMoveInv, an upper-triangular K, B >= M (the order-free score),
+// blob 0 finite (the NaN-at-origin test by one comparison).  Everything else: k_weigh_stream.
+template <typename T, int RNG, int MAXM, typename SP>
+constexpr bool kPkInstance = std::is_same<T, float>::value && RNG == kRngPhilox && MAXM == kExactM &&
+                             (std::is_same<SP, float>::value || std::is_same<SP, __half>::value);
+inline bool pk_eligible(const FrameArgsT<float>& fa) {
+  return fa.grid.on && fa.grid.b0fin && fa.small_angles && fa.cam_identity && fa.k_upper && fa.M == kExactM &&
+         fa.B >= fa.M && !(fa.diag & (kDiagNoPk | kDiagSortedScore));
+}
+template <typename T, int RNG, int MAXM, typename SP>
+inline const void* pk_kernel() {
+  if constexpr (kPkInstance<T, RNG, MAXM, SP>)
+    return (const void*)k_weigh_pk<SP>;
+  else
+    return nullptr;
+}
 
 template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
@@ -380,10 +401,15 @@ struct Seq {
     // partials (round 3: C3 116-117 -> 111-113 us per frame, profiles/r03/ab_c3_stream.log).
     // kDiagNoStream / kDiagForceStream pick either pass for tests and A/B.
     const bool stream = !(c->diag & kDiagNoStream);
-    c->last_weigh_pass = stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS;
+    // k_weigh_pk: the streaming pass with two particles per lane in packed fp32 (pf_weigh_pk.hpp), for the
+    // frames it covers (pk_eligible); same outputs, same bits
+    bool pk = false;
+    if constexpr (kPkInstance<T, RNG, MAXM, SP>) pk = stream && c->prune && pk_eligible(fa);
+    c->last_weigh_pass = pk ? PFMPE_WEIGH_PK : (stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS);
     if (stream) {
-      const void* fn = c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
-                                : (const void*)k_weigh_stream<T, RNG, MAXM, false, SP>;
+      const void* fn = pk ? pk_kernel<T, RNG, MAXM, SP>()
+                          : (c->prune ? (const void*)k_weigh_stream<T, RNG, MAXM, true, SP>
+                                      : (const void*)k_weigh_stream<T, RNG, MAXM, false, SP>);
       auto key = std::make_pair(fn, lds);
       auto it = c->occ.find(key);
       if (it == c->occ.end()) {
@@ -391,8 +417,16 @@ struct Seq {
         HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds));
         it = c->occ.emplace(key, std::max(1, per_cu)).first;
       }
-      const int grid = std::min(fa.nblk, it->second * std::max(1, c->num_cu));
+      // k_weigh_pk: a wave per 128-particle task, 2 * nblk tasks
+      const int grid = std::min(pk ? (fa.nblk + 1) / 2 : fa.nblk, it->second * std::max(1, c->num_cu));
       RET(launch_ext(c, PFMPE_K_PROPAGATE, [&] {
+        if constexpr (kPkInstance<T, RNG, MAXM, SP>) {
+          if (pk) {
+            klaunch(c, k_weigh_pk<SP>, dim3(grid), dim3(kBlock), lds, fa, table, prior, (float*)c->d_w[0],
+                    (float*)c->d_w[1], c->d_part[0], c->d_part[1], (const Ctrl*)c->d_ctrl, prop0, prop1, iter);
+            return;
+          }
+        }
         if (c->prune)
           klaunch(c, k_weigh_stream<T, RNG, MAXM, true, SP>, dim3(grid), dim3(kBlock), lds, fa,
                              table, prior, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1], c->d_ctrl, prop0,
@@ -577,6 +611,59 @@ struct Seq {
     last_args<T>(c) = fa;
     return PFMPE_OK;
   }
+  // A stream of a batch left no frame record.  If some descriptor failed the staging check (status != gen),
+  // report it as PFMPE_E_STATE with the words the device read that differ from the ones the host wrote (the
+  // HBM copy k_stage_multi made); otherwise it is the wait's own error.  No kernel followed a pointer of a
+  // failed descriptor, and a failed batch changes no context's prior (take_step is not reached).
+  static int batch_failure(pfmpe_ctx* c0, pfmpe_ctx* const* cs, const std::vector<int>& act,
+                           const std::vector<StreamDesc<T, SP>>& want, const unsigned char* ddesc, const uint32_t* dstat,
+                           uint32_t gen, const std::string& wait_err) {
+    using Desc = StreamDesc<T, SP>;
+    const int na = (int)act.size();
+    std::vector<uint32_t> st(na, 0);
+    std::vector<Desc> seen(na);
+    if (hipStreamSynchronize(c0->stream) != hipSuccess ||
+        hipMemcpy(st.data(), dstat, (size_t)na * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy((void*)seen.data(), ddesc, (size_t)na * sizeof(Desc), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(c0, PFMPE_E_HIP, "step_multi: " + wait_err);
+    static const std::pair<size_t, const char*> kFields[] = {
+        {offsetof(Desc, table), "table"},   {offsetof(Desc, prior), "prior"},   {offsetof(Desc, post), "post"},
+        {offsetof(Desc, w0), "w0"},         {offsetof(Desc, w1), "w1"},         {offsetof(Desc, part0), "part0"},
+        {offsetof(Desc, part1), "part1"},   {offsetof(Desc, bscan0), "bscan0"}, {offsetof(Desc, bscan1), "bscan1"},
+        {offsetof(Desc, gpart0), "gpart0"}, {offsetof(Desc, gpart1), "gpart1"}, {offsetof(Desc, gscan), "gscan"},
+        {offsetof(Desc, ctrl), "ctrl"},     {offsetof(Desc, gcount_w), "gcount_w"}, {offsetof(Desc, tcount_w), "tcount_w"},
+        {offsetof(Desc, gcount_r), "gcount_r"}, {offsetof(Desc, tcount_r), "tcount_r"}, {offsetof(Desc, prop0), "prop0"},
+        {offsetof(Desc, prop1), "prop1"},   {offsetof(Desc, cpart), "cpart"},   {offsetof(Desc, cgroup), "cgroup"},
+        {offsetof(Desc, counts), "counts"}, {offsetof(Desc, cand), "cand"},     {offsetof(Desc, mlpose), "mlpose"},
+        {offsetof(Desc, out), "out"},       {offsetof(Desc, seq), "seq|first_blk"}, {offsetof(Desc, gen), "gen"},
+        {offsetof(Desc, tag), "tag"},       {offsetof(FrameArgsT<T>, key0), "fa.key0|key1"},
+        {offsetof(FrameArgsT<T>, flo), "fa.flo|fhi"}};
+    auto name = [&](size_t off) -> std::string {
+      for (const auto& f : kFields)
+        if (f.first == off) return f.second;
+      return off < sizeof(FrameArgsT<T>) ? "fa+" + std::to_string(off) : "+" + std::to_string(off);
+    };
+    for (int i = 0; i < na; ++i) {
+      if (st[i] == gen) continue;
+      std::string msg = "step_multi: stream " + std::to_string(act[i]) + ": descriptor failed the staging check (gen " +
+                        std::to_string(gen) + ", status " + std::to_string(st[i]) + "); words read != written:";
+      const uint64_t* a = (const uint64_t*)&want[i];
+      const uint64_t* b = (const uint64_t*)&seen[i];
+      int shown = 0;
+      for (size_t k = 0; k < sizeof(Desc) / 8 && shown < 8; ++k)
+        if (a[k] != b[k]) {
+          char buf[96];
+          std::snprintf(buf, sizeof buf, " %s host 0x%llx device 0x%llx;", name(8 * k).c_str(), (unsigned long long)a[k],
+                        (unsigned long long)b[k]);
+          msg += buf;
+          ++shown;
+        }
+      if (!shown) msg += " none (the tag or generation check failed on words equal to the host's)";
+      cs[act[i]]->err = msg;
+      return fail(c0, PFMPE_E_STATE, msg);
+    }
+    return fail(c0, PFMPE_E_HIP, "step_multi: " + wait_err);
+  }
   // S contexts' frames as ONE batch on cs[0]'s HIP stream (pfmpe_step_multi): one weighing launch over every
   // stream's blocks, one resampling launch, one finishing launch with a block per stream.  Streams whose exit
   // rule did not fire on the first iteration get further iteration batches (the others are not relaunched),
@@ -597,10 +684,14 @@ struct Seq {
       int64_t total = 0;
       size_t lds_w = 0, lds_f = 0;
       bool all_kept = true;  // every stream has its kept propagated set: k_resample_multi<KEPT = true>
+      if (++c0->multi_gen == 0u || c0->multi_gen == ~0u) c0->multi_gen = 1u;  // never 0 / ~0 (status words)
+      const uint32_t gen = c0->multi_gen;
+      std::vector<Desc> want(na);  // the descriptors as written (the staging check's reference for a report)
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
         const FrameArgsT<T>& fa = fas[act[i]];
-        Desc& x = hd[i];
+        Desc& x = want[i];
+        std::memset((void*)&x, 0, sizeof(Desc));
         x.fa = fa;
         x.table = tables[act[i]];
         x.prior = (const SP*)c->d_state[c->prior_idx];
@@ -634,11 +725,16 @@ struct Seq {
         c->seq = (c->seq + 1) & 0x3fffffff;
         x.seq = c->seq;
         x.first_blk = (int32_t)total;
+        x.gen = gen;
+        x.tag = desc_tag((const uint64_t*)&x, (int)(offsetof(Desc, tag) / 8));
+        std::memcpy((void*)&hd[i], (const void*)&x, sizeof(Desc));
+        if (i == 0 && (c0->diag & kDiagCorruptDesc)) hd[0].fa.key0 ^= 1u;  // test: altered after the tag
         total += fa.nblk;
         lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.tbytes));
         lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
       }
       const BatchLayout Lt = batch_layout<Desc>(na, total, tbytes);
+      uint32_t* dstat = (uint32_t*)(d + Lt.soff);
       // iterations of this round: no launch past the largest remaining cap of the active streams (a launch past
       // a stream's own cap would be a no-op on its ctrl->done, but it also runs with an iteration number the
       // host's small-angle bound did not cover)
@@ -654,32 +750,35 @@ struct Seq {
       const uint16_t* db = (const uint16_t*)(d + Lt.boff);
       RET(launch_ext(c0, PFMPE_K_AUX, [&] {
         klaunch(c0, k_stage_multi<T, SP>, dim3((unsigned)na), dim3(kBlock), 0, hdev, d, (uint32_t)Lt.doff,
-                (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)Lt.boff);
+                (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)Lt.boff, dstat, gen);
       }));
       for (int k = 0; k < nit; ++k, ++iter) {
         RET(launch_ext(c0, PFMPE_K_PROPAGATE, [&] {
           if (c0->prune)
             klaunch(c0, k_propagate_weigh_multi<T, RNG, MAXM, true, SP>, dim3((unsigned)total), dim3(kBlock), lds_w, dd,
-                    db, na, iter);
+                    db, na, (const uint32_t*)dstat, gen, iter);
           else
             klaunch(c0, k_propagate_weigh_multi<T, RNG, MAXM, false, SP>, dim3((unsigned)total), dim3(kBlock), lds_w,
-                    dd, db, na, iter);
+                    dd, db, na, (const uint32_t*)dstat, gen, iter);
         }));
       }
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
         if (all_kept)
-          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
+          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
+                  (const uint32_t*)dstat, gen);
         else
-          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, false>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na);
+          klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, false>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
+                  (const uint32_t*)dstat, gen);
       }));
       RET(launch_ext(c0, PFMPE_K_FINAL, [&] {
-        klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd);
+        klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd,
+                (const uint32_t*)dstat, gen);
       }));
       std::vector<int> next;
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
         if (wait_frame(c, c0->stream) != PFMPE_OK)
-          return fail(c0, PFMPE_E_HIP, "step_multi: stream " + std::to_string(act[i]) + ": " + c->err);
+          return batch_failure(c0, cs, act, want, d + Lt.doff, dstat, gen, c->err);
         if (!frame_done(c)) next.push_back(act[i]);
       }
       if (next.empty()) break;
@@ -812,8 +911,6 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     return fail(c0, PFMPE_E_CAP, "step_multi: " + std::to_string(total) + " blocks in one batch (at most " +
                                      std::to_string(max_blocks) + " = " + std::to_string(max_blocks * kBlock) +
                                      " particles, PFMPE_OPT_MULTI_MAX_BLOCKS)");
-  // every member's work so far is ordered before the batch (its own stream, or an earlier batch led elsewhere)
-  for (int s = 0; s < S; ++s) RET(order_after(cs[s], c0->stream, c0));
   const size_t need = batch_layout<Desc>(S, total, tbytes).need;
   if (need > c0->multi_cap) {
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
@@ -832,6 +929,26 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   }
   for (int s = 0; s < S; ++s) RET(ensure_prop(cs[s]));
   RET((audit_batch<T, SP>(cs, S, fas.data(), in, toff, tbytes, total, c0->multi_cap)));
+  if (!c0->lead_fence) {  // created before any member's ordering state changes (no early return after)
+    auto f = std::make_shared<BatchFence>();
+    HIPCHK(c0, hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
+    c0->lead_fence = f;
+  }
+  // every member's work so far is ordered before the batch (its own stream, or an earlier batch led elsewhere).
+  // order_after clears a member's ordering state; if a later member's ordering fails, the earlier ones get their
+  // state back (their pending work is still unordered with their own streams)
+  {
+    std::vector<std::pair<hipStream_t, std::shared_ptr<BatchFence>>> saved(S);
+    for (int s = 0; s < S; ++s) saved[s] = {cs[s]->last_stream, cs[s]->last_fence};
+    for (int s = 0; s < S; ++s)
+      if (const int r = order_after(cs[s], c0->stream, c0)) {
+        for (int e = 0; e < S; ++e) {
+          cs[e]->last_stream = saved[e].first;
+          cs[e]->last_fence = saved[e].second;
+        }
+        return r;
+      }
+  }
   std::vector<const unsigned char*> tables(S);
   for (int s = 0; s < S; ++s) {
     pfmpe_ctx* c = cs[s];
@@ -851,18 +968,16 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     rc = Seq<T, RNG, 12, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
   else
     rc = Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
-  // the batch's kernels may still be retiring when the records are in: each member's next work on its own
-  // stream waits for the fence (the leader's own stream is the batch stream)
-  if (!c0->lead_fence) {
-    auto f = std::make_shared<BatchFence>();
-    HIPCHK(c0, hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
-    c0->lead_fence = f;
-  }
-  HIPCHK(c0, hipEventRecord(c0->lead_fence->ev, c0->stream));
+  // the batch's kernels may still be retiring when the records are in (or when a step failed part-way): each
+  // member's next work on its own stream waits for the fence (the leader's own stream is the batch stream).
+  // Set whatever step_multi returned; without a recorded fence a member orders after the batch stream itself
+  // (order_after records its own event there)
+  const bool fenced = hipEventRecord(c0->lead_fence->ev, c0->stream) == hipSuccess;
   for (int s = 0; s < S; ++s) {
     cs[s]->last_stream = c0->stream;
-    cs[s]->last_fence = s == 0 ? nullptr : c0->lead_fence;
+    cs[s]->last_fence = (s == 0 || !fenced) ? nullptr : c0->lead_fence;
   }
+  if (!fenced && rc == PFMPE_OK) return fail(c0, PFMPE_E_HIP, "step_multi: recording the batch fence failed");
   return rc;
 }
 

@@ -435,9 +435,10 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
+  const size_t ev_mark = c->ev_used;  // brackets of earlier frames still pending (harvested lazily)
   const int rs = dispatch_step(c, in, table, tbytes, gh);
   c->timing_now = false;
-  if (rs != PFMPE_OK) c->ev_used = 0;  // a failed frame's brackets are dropped
+  if (rs != PFMPE_OK) c->ev_used = ev_mark;  // only the failed frame's own brackets are dropped
   else if (c->ev_used >= kHarvestPairs) RET(harvest_timing(c));  // pending brackets: harvest_timing
   RET(rs);
   take_step(c, in, out);
@@ -464,6 +465,7 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
   RET(set_device(c0));
   c0->timing_now = c0->timing > 0 && (c0->timing_frame++ % c0->timing) == 0;  // batches timed on the leader
   const bool ref = c0->params.rng_mode == PFMPE_RNG_REFERENCE;
+  const size_t ev_mark = c0->ev_used;
   int rs;
   switch (c0->state_dtype) {
     case PFMPE_STATE_F64:
@@ -476,7 +478,7 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
       rs = ref ? multi_m<float, kRngReference, float>(ctxs, S, in) : multi_m<float, kRngPhilox, float>(ctxs, S, in);
   }
   c0->timing_now = false;
-  if (rs != PFMPE_OK) c0->ev_used = 0;
+  if (rs != PFMPE_OK) c0->ev_used = ev_mark;  // only the failed batch's own brackets are dropped
   else if (c0->ev_used >= kHarvestPairs) RET(harvest_timing(c0));
   RET(rs);
   for (int s = 0; s < S; ++s) {

@@ -680,9 +680,10 @@ int pfmpe_p3p_histogram(pfmpe_ctx* c, const double* blobs, int B, uint32_t* hist
   if (B > c->max_blobs) return fail(c, PFMPE_E_CAP, "p3p_histogram: B exceeds max_blobs");
   RET(set_device(c));
   c->timing_now = c->timing > 0;
+  const size_t ev_mark = c->ev_used;  // pending brackets of earlier frames
   const int rc = run_histogram(c, blobs, B, hist);
   c->timing_now = false;
-  c->ev_used = 0;
+  if (rc != PFMPE_OK) c->ev_used = ev_mark;  // only this call's brackets are dropped (success harvested them all)
   return rc;
 }
 

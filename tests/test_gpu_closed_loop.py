@@ -67,7 +67,10 @@ def run_pair(cfg, n_frames, state, rng, first_frame_check=None):
     if state != pf.STATE_F64:  # both loops start from the same (float-representable) set
         prior = prior.astype(np.float32).astype(np.float64)
     eng = _engine(cfg.N, st, state, rng, prior)
-    op = orc.make_params(rng_mode=rng)
+    if state == pf.STATE_F16:  # the oracle starts from the engine's own (fp16-delta quantised) prior
+        prior = eng.get_particles(1)
+    # fast_search: the oracle resampler's cumulative search by binary search (identical results, O(N log N))
+    op = orc.make_params(rng_mode=rng, fast_search=1)
     te, to = Tracker(st), Tracker(st)
     o_prior = prior
     rows = []
@@ -128,7 +131,7 @@ def test_closed_loop_c1_fp32():
 
 
 def test_closed_loop_c2_fp32_frame2():
-    """C2 (BASELINE.json configs[1]: 5 LEDs, 50 blobs, 100k particles, fp32) over 20 frames in the shape the
+    """C2 (BASELINE.json configs[1]: 5 LEDs, 50 blobs, 100k particles, fp32) over 60 frames in the shape the
     bench times (k_frame2: one launch, 391 blocks in 7 groups of 64).  The first frame, where both loops have
     the same inputs, is also compared particle by particle (the fp32 k_frame2 instantiation at
     this shape had only been compared with itself)."""
@@ -142,4 +145,18 @@ def test_closed_loop_c2_fp32_frame2():
         assert np.abs(prop - arr["propagated"]).max() < 1e-5
         assert out["iters"] == ref["iters"] and out["accepted"] == ref["accepted"]
 
-    assert_within(run_pair(syn.CONFIGS["C2"], 20, pf.STATE_F32, pf.RNG_PHILOX, first), 0.95, "C2 fp32")
+    assert_within(run_pair(syn.CONFIGS["C2"], 60, pf.STATE_F32, pf.RNG_PHILOX, first), 0.95, "C2 fp32")
+
+
+def test_closed_loop_c1_fp16():
+    """fp16-delta state (C4's storage) in the closed loop against the fp64 oracle loop:
+    C1's shape over 200 frames.  Each frame's resampled set is quantised to fp16 deltas against the frame's
+    current pose; the oracle keeps fp64 particles."""
+    assert_within(run_pair(syn.CONFIGS["C1"], 200, pf.STATE_F16, pf.RNG_PHILOX), 0.95, "C1 fp16")
+
+
+def test_closed_loop_100k_fp16():
+    """fp16-delta state at N = 100k (two launches are not forced: the shape the context picks) over 20 frames
+    against the fp64 oracle loop."""
+    cfg = syn.StreamConfig("C2f16", M=5, B=50, N=100_000)
+    assert_within(run_pair(cfg, 20, pf.STATE_F16, pf.RNG_PHILOX), 0.95, "100k fp16")

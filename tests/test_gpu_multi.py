@@ -348,3 +348,44 @@ def test_multi_interleaved_with_single_steps(state):
     finally:
         for e in mixed + solo:
             e.close()
+
+
+@pytest.mark.parametrize("state,rng", [(pf.STATE_F16, pf.RNG_PHILOX), (pf.STATE_F64, pf.RNG_REFERENCE)])
+def test_multi_corrupt_descriptor_is_reported(state, rng):
+    """a stream descriptor the device reads differently from what the host wrote is refused
+    before any of its pointers is followed.  PFMPE_DIAG 8192 alters the first stream's key word in the host image
+    after its tag was computed (a key word, never a pointer: nothing wild could be dereferenced even if the check
+    failed).  The batch must return PFMPE_E_STATE naming the differing word with both values; no context's prior
+    may change (the failed batch is as if it never ran), and the same contexts then batch normally and equal their
+    own pfmpe_step runs."""
+    cfgs = [(1000, 5, 20, False, ""), (4099, 5, 50, False, ""), (2048, 12, 200, True, "")]
+    streams = _streams(2, cfgs)
+    batch, solo = [], []
+    for (st, frames, how), (N, M, *_r) in zip(streams, cfgs):
+        for lst, fused in ((batch, 0), (solo, 2)):
+            eng = _engine(N, M, state, rng, fused=fused)
+            eng.set_prior(st.prior(N))
+            lst.append(eng)
+    try:
+        before = [e.get_particles(1) for e in batch]
+        batch[0].set_option(pf.OPT_DIAG, pf.DIAG_CORRUPT_DESC)
+        ins = [_frame(batch[s], streams[s][1][0][0], streams[s][1][0][1], "", 500 + s, 0) for s in range(len(cfgs))]
+        with pytest.raises(pf.PFError) as ei:
+            pf.Engine.step_multi(batch, ins)
+        assert ei.value.code == pf.E_STATE, str(ei.value)
+        msg = str(ei.value)
+        assert "stream 0" in msg and "staging check" in msg and "host 0x" in msg and "device 0x" in msg, msg
+        for e, b in zip(batch, before):
+            assert np.array_equal(e.get_particles(1), b)
+        batch[0].set_option(pf.OPT_DIAG, 0)
+        for f in range(2):
+            seeds = [700 + 3 * s + f for s in range(len(cfgs))]
+            ins = [_frame(batch[s], streams[s][1][f][0], streams[s][1][f][1], "", seeds[s], f) for s in range(len(cfgs))]
+            outs = pf.Engine.step_multi(batch, ins)
+            for s in range(len(cfgs)):
+                fr, blobs = streams[s][1][f]
+                ref = solo[s].step(_frame(solo[s], fr, blobs, "", seeds[s], f))
+                _same(_snapshot(batch[s], outs[s]), _snapshot(solo[s], ref), (state, s, f))
+    finally:
+        for e in batch + solo:
+            e.close()

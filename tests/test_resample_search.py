@@ -1,0 +1,84 @@
+"""CPU checks of the resampling test infrastructure (no GPU):
+
+* the oracle's fast_search option (binary search over the running max of the same sequential sums) gives the
+  reference scan's exact counts, indices and new prior (PE:668-682), including negative weights;
+* tests/stratified_ref.py's numpy Philox equals the oracle's Philox4x32-10 (itself pinned by the published
+  Random123 vectors in test_oracle_kat.py), and its exact O(N log N) assignment equals the oracle's O(N^2)
+  stratified_resample on random weights wherever no target is fragile.
+"""
+import numpy as np
+import pytest
+
+import pf_monocular_pose_estimator_amd.synthetic as syn
+from oracle import pforacle as orc
+import stratified_ref as sref
+
+
+@pytest.mark.parametrize("rng", [orc.RNG_REFERENCE, orc.RNG_PHILOX])
+def test_fast_search_equals_reference_scan(rng):
+    st = syn.make_stream(syn.CONFIGS["C1"], 3)
+    prior = st.prior()
+    for fr in st.frames:
+        res = []
+        for fast in (0, 1):
+            op = orc.make_params(rng_mode=rng, fast_search=fast)
+            res.append(orc.pf_step(st.markers, st.K, op, prior, fr.current_pose, fr.predicted_pose, fr.prediction,
+                                   fr.blobs, dt=fr.dt, seed=31 + fr.index, frame_idx=fr.index))
+        (ra, aa), (rb, ab) = res
+        assert ra["accepted"] == 1
+        for k in ra:
+            assert np.array_equal(np.asarray(ra[k]), np.asarray(rb[k])), k
+        for k in ("counts", "resample_idx", "resampled"):
+            assert np.array_equal(aa[k], ab[k]), k
+        prior = aa["resampled"]
+
+
+def test_fast_search_negative_weights():
+    """Self-occlusion penalties make weights negative; the cumulative sum is then non-monotone and the
+    first-reaching index is the running max's (SURVEY.md §7 hard part 3)."""
+    K = syn.K_README
+    s = 0.02
+    markers = np.array([[-s, -s, 0.0], [s, -s, 0.0], [s, s, 0.0], [-s, s, 0.0]])
+    T_true, T_far = np.eye(4), np.eye(4)
+    T_true[:3, 3] = [0.0, 0.0, 2.0]
+    T_far[:3, 3] = [0.0, 0.0, 40.0]
+    blobs = np.vstack([syn.project(K, T_true, markers),
+                       (syn.project(K, T_far, markers).mean(axis=0) + np.array([3.4, 0.0]))[None]])
+    prior = np.array([syn.to12(T_true if n % 3 else T_far) for n in range(64)])
+    ident = np.eye(4)[:3].reshape(12)
+    res = []
+    for fast in (0, 1):
+        op = orc.make_params(ang=(0.0, 0.0), trans=(0.0, 0.0), rng_mode=orc.RNG_PHILOX, fast_search=fast)
+        res.append(orc.pf_step(markers, K, op, prior, syn.to12(T_true), syn.to12(T_true), ident, blobs,
+                               it_since_init=1, seed=3))
+    (ra, aa), (rb, ab) = res
+    assert (aa["weights"] < 0).any() and ra["accepted"] == 1
+    for k in ("counts", "resample_idx", "resampled"):
+        assert np.array_equal(aa[k], ab[k]), k
+    assert ra["winner_idx"] == rb["winner_idx"]
+
+
+def test_numpy_philox_equals_oracle():
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        ctr = rng.integers(0, 2 ** 32, size=4, dtype=np.uint64)
+        key = rng.integers(0, 2 ** 32, size=2, dtype=np.uint64)
+        want = orc.philox(ctr.astype(np.uint32), key.astype(np.uint32))
+        got = sref.philox4x32_10(*(np.array([c]) for c in ctr), int(key[0]), int(key[1]))
+        assert [int(g[0]) for g in got] == [int(x) for x in want]
+
+
+@pytest.mark.parametrize("N,neg", [(1000, False), (3000, True), (4096, False)])
+def test_exact_assignment_matches_oracle_scan(N, neg):
+    """On fp32-valued weights the oracle's sequential fp64 scan and the extended-precision assignment agree on
+    every non-fragile target; fragile ones (if any) stay within the allowed set."""
+    rng = np.random.default_rng(N)
+    w = rng.uniform(0.0, 30.0, size=N).astype(np.float32).astype(np.float64)
+    w[rng.choice(N, N // 4, replace=False)] = 0.0  # particles with no accepted marker
+    if neg:
+        w[rng.choice(N, N // 50, replace=False)] = -rng.uniform(0.5, 9.0, size=N // 50).astype(np.float32)
+    seed, frame = 12345 + N, 7
+    counts, _ = orc.stratified_resample(w, orc.RNG_PHILOX, seed, frame, 1)
+    r = sref.philox_targets(N, seed, frame)
+    stats = sref.compare_counts(counts, w, r)
+    assert stats["differing"] == 0  # the oracle's own fp64 roundings sit far inside delta at these sizes
