@@ -326,11 +326,15 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *                                  two-launch frames (0: stay off)
  *   PFMPE_OPT_MULTI_MAX_BLOCKS [160000|1..160000] largest pfmpe_step_multi batch this context leads, in
  *                                  256-particle blocks (PFMPE_E_CAP above); the default is the tested limit
+ *   PFMPE_OPT_DEFER_RESAMPLE [1|0] two-launch frames with the kept propagated set: resampling writes each
+ *                                  slot's owner index (4 B) instead of gathering and scattering the particle,
+ *                                  and the next frame reads the prior through those indices.
+ *                                  Results are bit-identical either way (pfmpe_get_particles gathers)
  * Within one process at most one one-launch frame runs per device at a time: a context that finds another
  * context's one-launch frame in flight on its device runs that frame as two launches (PFMPE_INFO_GUARD_SKIPS). */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4,
        PFMPE_OPT_KEEP_PROPAGATED = 5, PFMPE_OPT_WAIT_BOUND_US = 6, PFMPE_OPT_FUSED_REARM = 7,
-       PFMPE_OPT_MULTI_MAX_BLOCKS = 8 };
+       PFMPE_OPT_MULTI_MAX_BLOCKS = 8, PFMPE_OPT_DEFER_RESAMPLE = 9 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* Context state for monitoring and tests (no reference counterpart: engine introspection). */

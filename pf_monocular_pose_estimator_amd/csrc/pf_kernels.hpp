@@ -121,6 +121,12 @@ struct FrameArgsT {
   GridArgs grid;                  // the table's 2D grid (fp32 pruned column minima)
   int64_t ld;                     // SoA plane stride in elements
   T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
+  // Deferred resampling: the prior may be stored as an earlier frame's kept propagated set plus
+  // owner indices, prior particle n = stored particle owner[n] (null: stored in particle order).  owner_out
+  // (two-launch frames with the kept set): k_resample writes the new prior's owner indices there instead of
+  // gathering and scattering the particles (null: the new prior is materialised in the post buffer).
+  const uint32_t* owner;
+  uint32_t* owner_out;
 };
 
 // The frame-constant arrays, staged once per block into LDS and read from there (broadcast reads):
@@ -526,10 +532,15 @@ __device__ __forceinline__ T state_from_raw(const RawState<SP>& R, int q, T anch
 }
 
 // prior particle n (SoA planes), loaded ahead of use so the loads overlap other work
+// the stored row of prior particle n (deferred prior: its owner index)
+template <typename T>
+__device__ __forceinline__ int prior_row(const FrameArgsT<T>& fa, int n) {
+  return fa.owner ? (int)fa.owner[n] : n;
+}
 template <typename T, typename SP>
 __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __restrict__ prior, int n, T* A) {
   SP v[12];
-  load_state_raw<SP>(prior, fa.ld, n, v);
+  load_state_raw<SP>(prior, fa.ld, prior_row(fa, n), v);
 #pragma unroll
   for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(v[q], fa.anc_in[q]);
 }
@@ -1491,8 +1502,9 @@ enum : int {
   kDiagForceStream = 1024, // two-launch path: always the streaming weighing pass (tests / A/B)
   kDiagSerialTop = 2048,   // streaming pass with > 64 groups: the one-wave k_top instead of k_top_wide (A/B)
   kDiagNoPk = 4096,        // two-launch path: never the two-particles-per-lane pass k_weigh_pk (A/B, tests)
-  kDiagCorruptDesc = 8192  // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
+  kDiagCorruptDesc = 8192, // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
                            // staging check; the altered word is a key word, never a pointer)
+  kDiagNoDefer = 16384     // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -2354,7 +2366,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   RawState<SP> R{};
   {
     const int n = vb * kBlock + (int)threadIdx.x;
-    load_state_prefetch<SP>(prior, fa.ld, in_planes(n, fa.N), n < fa.N && n >= 2, R);
+    load_state_prefetch<SP>(prior, fa.ld, prior_row(fa, in_planes(n, fa.N)), n < fa.N && n >= 2, R);
   }
   stage_consts(fa, sc);
   __syncthreads();  // table + constants visible
@@ -2366,7 +2378,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     T A[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) A[q] = state_from_raw<T, SP>(R, q, fa.anc_in[q]);
-    load_state_prefetch<SP>(prior, fa.ld, in_planes(n + step, fa.N), n + step < fa.N && n + step >= 2, R);  // next block
+    load_state_prefetch<SP>(prior, fa.ld, prior_row(fa, in_planes(n + step, fa.N)), n + step < fa.N && n + step >= 2,
+                            R);  // next block
     T w = (T)0, P[12];
     if (valid) w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P);
     if (valid) {
@@ -2430,10 +2443,9 @@ __global__ __launch_bounds__(64) void k_group_top(const FrameArgsT<T> fa, BlockP
 }
 
 template <typename T, int RNG>
-__global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
-                                            GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
-                                            Ctrl* __restrict__ ctrl, int iter, int lds_groups) {
-  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // lds_groups: ngrp entries
+__device__ __forceinline__ void top_body(const FrameArgsT<T>& fa, GroupPart* __restrict__ gpart0,
+                                         GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                         Ctrl* __restrict__ ctrl, int iter, int lds_groups, GroupPart* gsm) {
   if (ctrl->done) return;
   const int slot = ctrl->cur_slot;
   const GroupPart* src = slot ? gpart1 : gpart0;
@@ -2466,6 +2478,13 @@ __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* _
   }
   propagate_top<T, RNG>(fa, ctrl, iter, gpart0, gpart1, gscan, nullptr, 0u, g0, single, slot, staged);
 }
+template <typename T, int RNG>
+__global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
+                                            GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                            Ctrl* __restrict__ ctrl, int iter, int lds_groups) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // lds_groups: ngrp entries
+  top_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, lds_groups, gsm);
+}
 
 // ---- k_top for more than one tile of groups (ngrp > 64, partials staged in LDS): 16 waves instead of one.
 // The per-tile work of propagate_top's final-iteration passes (the tile's inclusive sum, its G_g, the
@@ -2478,15 +2497,20 @@ __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* _
 // run propagate_top itself in wave 0.
 constexpr int kTopWaves = 16;
 constexpr int kTopMaxTiles = 24;  // ngrp <= 1365 (staged) -> <= 22 tiles
+struct TopWideLds {
+  double tileT[kTopMaxTiles], tileM[kTopMaxTiles], carryT[kTopMaxTiles];
+  double S_sh;
+  int wide;
+};
 template <typename T, int RNG>
-__global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
-                                                          GroupPart* __restrict__ gpart1,
-                                                          GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
-                                                          int iter) {
-  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries
-  __shared__ double tileT[kTopMaxTiles], tileM[kTopMaxTiles], carryT[kTopMaxTiles];
-  __shared__ double S_sh;
-  __shared__ int wide;
+__device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart* __restrict__ gpart0,
+                                              GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan,
+                                              Ctrl* __restrict__ ctrl, int iter, GroupPart* gsm, TopWideLds& tw) {
+  double* tileT = tw.tileT;
+  double* tileM = tw.tileM;
+  double* carryT = tw.carryT;
+  double& S_sh = tw.S_sh;
+  int& wide = tw.wide;
   if (ctrl->done) return;  // uniform
   const int slot = ctrl->cur_slot;
   const GroupPart* src = slot ? gpart1 : gpart0;
@@ -2608,6 +2632,15 @@ __global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T>
   }
   if (lane == 0) store_ctrl_wt(ctrl, c);
 }
+template <typename T, int RNG>
+__global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T> fa, GroupPart* __restrict__ gpart0,
+                                                          GroupPart* __restrict__ gpart1,
+                                                          GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+                                                          int iter) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries
+  __shared__ TopWideLds tw;
+  top_wide_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, gsm, tw);
+}
 
 // ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread.
 // One block's work (block `blk` of its stream), shared by the one-stream kernel and the batched kernel
@@ -2718,6 +2751,8 @@ struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B wor
   RecOut* out;
   int32_t seq;
   int32_t first_blk;  // the stream's first block in the grid
+  int32_t wg;         // resident workgroups of the stream in a streaming batched weighing pass (k_weigh_pk_multi)
+  int32_t pad_wg;
   uint64_t gen;       // the batch generation (staging launch counter; every kernel of the round gets it)
   uint64_t tag;       // desc_tag over every word before this one (pf_desc_tag.hpp)
 };
@@ -3173,7 +3208,13 @@ __device__ __forceinline__ void resample_phase(
   const int we = lane_value(e, 63);
   auto& rows = sh.rows[wv];
   uint2* rraw = (uint2*)&rows[0];  // RAWROW: three 8-B words per row
-  if constexpr (RAWROW) {
+  // Deferred resampling (two-launch frames with the kept set, MODE 0, fa.owner_out set): the new prior is the
+  // kept set read through owner indices, so the scatter writes slot k's owner (a particle index, 4 B) instead of
+  // the particle (S bytes), and nothing is staged: the next frame's weighing pass gathers kept[owner[k]].
+  const bool owners = MODE == 0 && RAW && fa.owner_out != nullptr;  // wave-uniform
+  if (owners) {
+    // (no rows: k_resample_final regenerates the winner, as for every RAW frame)
+  } else if constexpr (RAWROW) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
       rraw[3 * lane + j] = make_uint2(__builtin_bit_cast(uint32_t, raw_in->p[2 * j]),
@@ -3198,7 +3239,9 @@ __device__ __forceinline__ void resample_phase(
       carry = lane_value(own, 63);
       const int k = base + lane;
       wave_lds_sync();  // rows (before the loop) and this chunk's map reads are done before the next clear
-      if (k < we) {
+      if (k < we && owners) {
+        fa.owner_out[k] = (uint32_t)(blk * kBlock + wv * 64 + own);
+      } else if (k < we) {
         if constexpr (RAWROW) {
           uint32_t w6[6];
 #pragma unroll
@@ -3353,7 +3396,8 @@ __device__ __forceinline__ void resample_block(
   // the kept iteration's stored propagated set, gathered as raw state values (no regeneration).  fp16: planes
   // 2j and 2j + 1 are word j (one dword of the pair plane), which is the row layout resample_phase stages
   RawState<SP> KR{};
-  if (kept) {
+  // deferred resampling writes owner indices only: the kept set is not read here (fa.owner_out uniform)
+  if (kept && !fa.owner_out) {
     const SP* src = c.kept_slot ? prop1 : prop0;
     // buffer-resource planes: every lane loads (a lane past N at the index clamped into [0, N), in_planes), so
     // no branch: behind one, the weights' wait before the block scan became vmcnt(0) and also waited for these
@@ -4094,11 +4138,12 @@ __global__ void k_import(const double* __restrict__ poses, SP* __restrict__ st, 
 }
 template <typename T, typename SP>
 __global__ void k_export(const SP* __restrict__ st, double* __restrict__ poses, int N, int64_t ld,
-                         const Pose12<T> anchor) {
+                         const Pose12<T> anchor, const uint32_t* __restrict__ owner) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
+  const int r = owner ? (int)owner[n] : n;  // a deferred prior: stored row owner[n]
   for (int q = 0; q < 12; ++q)
-    poses[12 * (int64_t)n + q] = (double)StateIO<T, SP>::load(st[plane_index<SP>(q, n, ld)], anchor.v[q]);
+    poses[12 * (int64_t)n + q] = (double)StateIO<T, SP>::load(st[plane_index<SP>(q, r, ld)], anchor.v[q]);
 }
 template <typename T, int RNG, typename SP>
 __global__ __launch_bounds__(kBlock) void k_regen(const FrameArgsT<T> fa, int kept_iter, const SP* __restrict__ prior,
@@ -4122,6 +4167,7 @@ struct RoiArgs {
   double cam[12], predm[12], K[9], markers[kMaxMarkers * 3], anchor[12];
   int32_t N, M;
   int64_t ld;
+  const uint32_t* owner;  // a deferred prior's owner indices (FrameArgsT::owner), or null
 };
 template <typename T, typename SP>
 __global__ __launch_bounds__(kBlock) void k_roi(const RoiArgs ra, const SP* __restrict__ prior,
@@ -4131,9 +4177,10 @@ __global__ __launch_bounds__(kBlock) void k_roi(const RoiArgs ra, const SP* __re
   double xmin = INFINITY, xmax = 0.0, ymin = INFINITY, ymax = 0.0;
   if (n < ra.N) {
     double A[12], X[12], P[12];
+    const int r = ra.owner ? (int)ra.owner[n] : n;
 #pragma unroll
     for (int q = 0; q < 12; ++q)
-      A[q] = (double)StateIO<T, SP>::load(prior[plane_index<SP>(q, n, ra.ld)], (T)ra.anchor[q]);
+      A[q] = (double)StateIO<T, SP>::load(prior[plane_index<SP>(q, r, ra.ld)], (T)ra.anchor[q]);
     compose(ra.cam, A, X);   // camMoveInv * newPoseEstimation[j]
     compose(X, ra.predm, P); // ... * predictionMatrix
     double Q[12];

@@ -290,32 +290,46 @@ __device__ __forceinline__ uint32_t sopaque(uint32_t x) {
 #define PFMPE_WEIGH_PK_MIN_WAVES 1
 #endif
 
-template <typename SP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_PK_MIN_WAVES))) void k_weigh_pk(
-    const FrameArgsT<float> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
-    float* __restrict__ w0, float* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
-    const Ctrl* __restrict__ ctrl, SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
+// The pass for one stream: workgroup wg of nwg resident workgroups (the one-stream kernel: blockIdx / gridDim; the
+// batched kernel: the stream's share of the grid).  fa_words: the frame arguments as words (kernarg segment or the
+// stream's descriptor) for the LDS constants.
+template <typename SP, bool MULTI>
+__device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const uint32_t* fa_words, int wg, int nwg,
+                                              const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+                                              float* __restrict__ w0, float* __restrict__ w1,
+                                              BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+                                              const Ctrl* __restrict__ ctrl, SP* __restrict__ prop0,
+                                              SP* __restrict__ prop1, int iter, unsigned char* smem,
+                                              LdsConst<float>& sc, PkLds& pl) {
   constexpr int MAXM = kExactM;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ LdsConst<float> sc;
-  __shared__ PkLds pl;
-  if (ctrl->done) return;  // the exit rule already fired (uniform)
-  const int slot = ctrl->cur_slot;
+  // the exit rule already fired (uniform); this iteration's weight slot (batched: explicit scalar loads of a
+  // record written by an earlier launch, pf_kernels.hpp load_ctrl_word)
+  if (MULTI ? load_ctrl_word<(int)offsetof(Ctrl, done)>(ctrl) : ctrl->done) return;
+  const int slot = MULTI ? load_ctrl_word<(int)offsetof(Ctrl, cur_slot)>(ctrl) : ctrl->cur_slot;
   float* wout = slot ? w1 : w0;
   SP* pout = slot ? prop1 : prop0;
   BlockPart* parts = slot ? part1 : part0;
   const int lane = lane_id();
   const int ntask = 2 * fa.nblk;  // 128-particle tasks: every wave partial slot 4 * nblk gets written
-  const int nwaves = (int)gridDim.x * kWaves;
-  int tk = (int)blockIdx.x * kWaves + wave_id_u();
+  const int nwaves = nwg * kWaves;
+  int tk = wg * kWaves + wave_id_u();
   copy_table(table, smem, (size_t)fa.tbytes);
+  // stored rows of a task's two particles: n itself, or owner[n] for a deferred prior (FrameArgsT::owner).  The
+  // owner indices are loaded one task ahead of the state they address (software pipelining: the state loads of
+  // task t + 1, issued while task t computes, use owner values that arrived during task t - 1)
+  const uint32_t* own = fa.owner;
+  auto rows_of = [&](int t, int& ra, int& rb) {
+    const int n = in_planes(t * 128 + lane, fa.N), m = in_planes(t * 128 + 64 + lane, fa.N);
+    ra = own ? (int)own[n] : n;
+    rb = own ? (int)own[m] : m;
+  };
   Raw2<SP> R{};
-  {
-    const int n = tk * 128 + lane;
-    load_state_prefetch<SP>(prior, fa.ld, in_planes(n, fa.N), true, R.a);
-    load_state_prefetch<SP>(prior, fa.ld, in_planes(n + 64, fa.N), true, R.b);
-  }
-  stage_consts(fa, sc);
+  int rA, rB;
+  rows_of(tk, rA, rB);
+  load_state_prefetch<SP>(prior, fa.ld, rA, true, R.a);
+  load_state_prefetch<SP>(prior, fa.ld, rB, true, R.b);
+  rows_of(tk + nwaves, rA, rB);
+  stage_consts_from(fa_words, sc);
   if (threadIdx.x < 12) {
     pl.anc_in[threadIdx.x] = fa.anc_in[threadIdx.x];
     pl.anc_out[threadIdx.x] = fa.anc_out[threadIdx.x];
@@ -342,11 +356,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     // the plane stride, re-derived each task on the scalar unit (hoisted, its plane offsets held SGPRs across the
     // loop and spilled)
     const int64_t ldl = (int64_t)sopaque((uint32_t)fa.ld);
-    {  // the next task's state, in flight across this task's arithmetic
-      const int n = (tk + nwaves) * 128 + lane;
-      load_state_prefetch<SP>(prior, ldl, in_planes(n, fa.N), true, R.a);
-      load_state_prefetch<SP>(prior, ldl, in_planes(n + 64, fa.N), true, R.b);
-    }
+    // the next task's state, in flight across this task's arithmetic; then the rows of the task after it
+    load_state_prefetch<SP>(prior, ldl, rA, true, R.a);
+    load_state_prefetch<SP>(prior, ldl, rB, true, R.b);
+    rows_of(tk + 2 * nwaves, rA, rB);
     // ---- motion model (propagate, PE:543-588), both particles per instruction
     const Phx2 ph = philox_motion_pair((uint32_t)nA, (uint32_t)nB, (uint32_t)iter | (kTagMotion << 24), fa.flo, fa.fhi,
                                        fa.key0, fa.key1);
@@ -522,6 +535,96 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
     pk_wave_partial(wA, vA, tk * 128, parts + (size_t)tk * 2);
     pk_wave_partial(wB, vB, tk * 128 + 64, parts + (size_t)tk * 2 + 1);
   }
+}
+
+template <typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_PK_MIN_WAVES))) void k_weigh_pk(
+    const FrameArgsT<float> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    float* __restrict__ w0, float* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    const Ctrl* __restrict__ ctrl, SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<float> sc;
+  __shared__ PkLds pl;
+  weigh_pk_body<SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x,
+                           (int)gridDim.x, table, prior, w0, w1, part0, part1, ctrl, prop0, prop1, iter, smem, sc, pl);
+}
+
+// ---- batched streams (pfmpe_step_multi): the streaming packed pass for every stream of a batch in ONE launch.
+// Grid (max wg, streams): workgroup (x, s) is workgroup x of the desc.wg resident workgroups the host gave stream
+// s (its share of the device's resident capacity, in proportion to its particles), so a workgroup stages one
+// stream's table and constants once and loops over that stream's tasks only: each stream computes exactly its
+// one-stream k_weigh_pk.  A stream whose descriptor failed the staging check (status != gen) is skipped.
+template <typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_PK_MIN_WAVES))) void k_weigh_pk_multi(
+    const StreamDesc<float, SP>* __restrict__ descs, int S, const uint32_t* __restrict__ status, uint32_t gen,
+    int iter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<float> sc;
+  __shared__ PkLds pl;
+  const int s = (int)blockIdx.y;
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<float, SP>& d = descs[s];
+  const int nwg = __builtin_amdgcn_readfirstlane(d.wg);
+  if ((int)blockIdx.x >= nwg) return;
+  weigh_pk_body<SP, true>(d.fa, (const uint32_t*)&d.fa, (int)blockIdx.x, nwg, d.table, d.prior, d.w0, d.w1, d.part0,
+                          d.part1, d.ctrl, d.prop0, d.prop1, iter, smem, sc, pl);
+}
+
+// ---- the batched streaming pass's group / top hand-off (k_group_top / k_group + k_top_wide / k_top of every
+// stream of the batch, one launch each): grid (max groups, streams) for the group scans, (streams) for the tops.
+// The bodies are the one-stream kernels' (same functions, same association), with the stream's frame arguments,
+// buffers and counters from its descriptor; blocks past a stream's groups, and streams that failed the staging
+// check, return at once.
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(64) void k_group_top_multi(const StreamDesc<T, SP>* __restrict__ descs, int S,
+                                                        const uint32_t* __restrict__ status, uint32_t gen, int iter) {
+  const int s = (int)blockIdx.y;
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  const int g = (int)blockIdx.x;
+  const int ngrp = __builtin_amdgcn_readfirstlane(d.fa.ngrp);
+  if (g >= ngrp) return;
+  Ctrl* ctrl = d.ctrl;
+  if (load_ctrl_word<(int)offsetof(Ctrl, done)>(ctrl)) return;  // every block reads ctrl before it arrives
+  const int slot = load_ctrl_word<(int)offsetof(Ctrl, cur_slot)>(ctrl);
+  const GroupPart gr = propagate_group<true>(__builtin_amdgcn_readfirstlane(d.fa.nblk), __builtin_amdgcn_readfirstlane(d.fa.gsz),
+                                             g, slot ? d.part1 : d.part0, slot ? d.bscan1 : d.bscan0,
+                                             slot ? d.gpart1 : d.gpart0);
+  const bool single = ngrp == 1;
+  if (!single && !wave_arrive_last(d.tcount_w, ngrp)) return;
+  propagate_top<T, RNG>(d.fa, ctrl, iter, d.gpart0, d.gpart1, d.gscan, nullptr, 0u, gr, single, slot);
+}
+template <typename T, typename SP>
+__global__ __launch_bounds__(64) void k_group_multi(const StreamDesc<T, SP>* __restrict__ descs, int S,
+                                                    const uint32_t* __restrict__ status, uint32_t gen) {
+  const int s = (int)blockIdx.y;
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  const int g = (int)blockIdx.x;
+  if (g >= __builtin_amdgcn_readfirstlane(d.fa.ngrp)) return;
+  if (load_ctrl_word<(int)offsetof(Ctrl, done)>(d.ctrl)) return;
+  const int slot = load_ctrl_word<(int)offsetof(Ctrl, cur_slot)>(d.ctrl);
+  (void)propagate_group<true>(__builtin_amdgcn_readfirstlane(d.fa.nblk), __builtin_amdgcn_readfirstlane(d.fa.gsz), g,
+                              slot ? d.part1 : d.part0, slot ? d.bscan1 : d.bscan0, slot ? d.gpart1 : d.gpart0);
+}
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(64 * kTopWaves) void k_top_wide_multi(const StreamDesc<T, SP>* __restrict__ descs, int S,
+                                                                const uint32_t* __restrict__ status, uint32_t gen,
+                                                                int iter) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // the largest stream's ngrp entries
+  __shared__ TopWideLds tw;
+  const int s = (int)blockIdx.x;
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  top_wide_body<T, RNG>(d.fa, d.gpart0, d.gpart1, d.gscan, d.ctrl, iter, gsm, tw);
+}
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(64) void k_top_multi(const StreamDesc<T, SP>* __restrict__ descs, int S,
+                                                  const uint32_t* __restrict__ status, uint32_t gen, int iter) {
+  const int s = (int)blockIdx.x;
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  top_body<T, RNG>(d.fa, d.gpart0, d.gpart1, d.gscan, d.ctrl, iter, 0, nullptr);
 }
 
 }  // namespace pfmpe

@@ -60,6 +60,14 @@ struct pfmpe_ctx {
   int prior_idx = 0;
   void* d_w[2] = {nullptr, nullptr};
   void* d_prop[2] = {nullptr, nullptr};  // two-launch path: propagated set per weight slot (keep_prop)
+  // Deferred resampling (PFMPE_OPT_DEFER_RESAMPLE): a two-launch frame with the kept set writes the
+  // new prior's owner indices (d_owner[frame_owner_out]) instead of the particles; the frame's kept buffer then
+  // becomes the prior's storage (swapped with the unused post buffer at take_step) and prior particle n is stored
+  // row d_owner[prior_owner][n].  prior_owner = -1: the prior is stored in particle order.
+  uint32_t* d_owner[2] = {nullptr, nullptr};
+  int prior_owner = -1;
+  int frame_owner_out = -1;  // this frame's owner buffer (-1: materialised resample)
+  bool defer = true;
   int max_grp = 0;
   BlockPart* d_part[2] = {nullptr, nullptr};
   BlockScan* d_bscan[2] = {nullptr, nullptr};
@@ -340,10 +348,18 @@ template <> inline FrameArgsT<double>& last_args<double>(pfmpe_ctx* c) { return 
 // the two-launch path's propagated-set buffers (PFMPE_OPT_KEEP_PROPAGATED), allocated on first use: the
 // one-launch frames keep the propagated particle in registers and never need them
 inline int ensure_prop(pfmpe_ctx* c) {
-  if (!c->keep_prop || c->d_prop[0]) return PFMPE_OK;
-  const size_t bytes = (size_t)kPlanes * c->ld * c->es;
-  for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&c->d_prop[i], bytes));
+  if (!c->keep_prop) return PFMPE_OK;
+  if (!c->d_prop[0]) {
+    const size_t bytes = (size_t)kPlanes * c->ld * c->es;
+    for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&c->d_prop[i], bytes));
+  }
+  if (c->defer && !c->d_owner[0])
+    for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc((void**)&c->d_owner[i], (size_t)c->ld * sizeof(uint32_t)));
   return PFMPE_OK;
+}
+// the owner indices of the current prior (null: stored in particle order)
+inline const uint32_t* prior_owner_ptr(const pfmpe_ctx* c) {
+  return c->prior_owner >= 0 ? c->d_owner[c->prior_owner] : nullptr;
 }
 
 // Batch scratch layout (pfmpe_step_multi), the same in the pinned host image and in HBM: host-supplied blob
@@ -476,10 +492,17 @@ struct Seq {
     c->seq = (c->seq + 1) & 0x3fffffff;
     const int32_t seq = c->seq;
     const bool kept = c->keep_prop && c->d_prop[0];  // iterate() allocated them
+    // deferred resampling: the new prior's owner indices go to the owner buffer the current prior does not use
+    FrameArgsT<T> far = fa;
+    c->frame_owner_out = -1;
+    if (kept && c->defer && c->d_owner[0] && !(c->diag & kDiagNoDefer)) {
+      c->frame_owner_out = c->prior_owner == 0 ? 1 : 0;
+      far.owner_out = c->d_owner[c->frame_owner_out];
+    }
     RET(launch_ext(c, PFMPE_K_RESAMPLE, [&] {
       // the kept-set variant compiles the regeneration path out (its registers spilled in the generic form)
       auto k = kept ? k_resample<T, RNG, MAXM, SP, true> : k_resample<T, RNG, MAXM, SP, false>;
-      klaunch(c, k, dim3(fa.nblk), dim3(kBlock), 0, fa, c->d_ctrl, table,
+      klaunch(c, k, dim3(fa.nblk), dim3(kBlock), 0, far, c->d_ctrl, table,
                          prior, post, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0], c->d_bscan[1],
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
@@ -733,6 +756,40 @@ struct Seq {
         lds_w = std::max(lds_w, BlobTable<T>::lds_bytes(fa.tbytes));
         lds_f = std::max(lds_f, BlobTable<T>::bytes(fa.B));
       }
+      // The streaming packed pass for the whole batch (k_weigh_pk_multi + the batched group / top hand-off) when
+      // every stream's frame is one k_weigh_pk covers; otherwise the one-block pass with its in-launch hand-off
+      // (k_propagate_weigh_multi).  Each stream gets a share of the resident workgroups in proportion to its
+      // particles (at least one, at most one per four tasks), written into its descriptor before the tag.
+      bool pk = false;
+      int pk_grid_x = 0, max_ngrp = 0;
+      if constexpr (kPkInstance<T, RNG, MAXM, SP>) {
+        pk = c0->prune && !(c0->diag & (kDiagNoStream | kDiagNoPk));
+        for (int i = 0; i < na && pk; ++i) pk = pk_eligible(fas[act[i]]);
+        if (pk) {
+          const void* fn = (const void*)k_weigh_pk_multi<SP>;
+          auto key = std::make_pair(fn, lds_w);
+          auto it = c0->occ.find(key);
+          if (it == c0->occ.end()) {
+            int per_cu = 0;
+            HIPCHK(c0, hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds_w));
+            it = c0->occ.emplace(key, std::max(1, per_cu)).first;
+          }
+          const int64_t cap = (int64_t)it->second * std::max(1, c0->num_cu);
+          for (int i = 0; i < na; ++i) {
+            const FrameArgsT<T>& fa = fas[act[i]];
+            const int64_t tasks = 2 * (int64_t)fa.nblk;
+            const int64_t share = std::max<int64_t>(1, cap * fa.nblk / std::max<int64_t>(1, total));
+            const int wg = (int)std::max<int64_t>(1, std::min<int64_t>(share, (tasks + kWaves - 1) / kWaves));
+            Desc& x = want[i];
+            x.wg = wg;
+            x.tag = desc_tag((const uint64_t*)&x, (int)(offsetof(Desc, tag) / 8));
+            std::memcpy((void*)&hd[i], (const void*)&x, sizeof(Desc));
+            if (i == 0 && (c0->diag & kDiagCorruptDesc)) hd[0].fa.key0 ^= 1u;
+            pk_grid_x = std::max(pk_grid_x, wg);
+            max_ngrp = std::max(max_ngrp, fa.ngrp);
+          }
+        }
+      }
       const BatchLayout Lt = batch_layout<Desc>(na, total, tbytes);
       uint32_t* dstat = (uint32_t*)(d + Lt.soff);
       // iterations of this round: no launch past the largest remaining cap of the active streams (a launch past
@@ -753,6 +810,33 @@ struct Seq {
                 (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)Lt.boff, dstat, gen);
       }));
       for (int k = 0; k < nit; ++k, ++iter) {
+        if constexpr (kPkInstance<T, RNG, MAXM, SP>) {
+          if (pk) {
+            const uint32_t* cst = dstat;
+            RET(launch_ext(c0, PFMPE_K_PROPAGATE, [&] {
+              klaunch(c0, k_weigh_pk_multi<SP>, dim3((unsigned)pk_grid_x, (unsigned)na), dim3(kBlock), lds_w, dd, na,
+                      cst, gen, iter);
+            }));
+            // the group / top hand-off: one launch when every stream's groups fit one tile, else group scans +
+            // the wide top (group partials staged in LDS) or, beyond its LDS, the one-wave top
+            const size_t glds = (size_t)max_ngrp * sizeof(GroupPart);
+            const bool wide = glds <= 64 * 1024 && max_ngrp <= 64 * kTopMaxTiles && !(c0->diag & kDiagSerialTop);
+            RET(launch_ext(c0, PFMPE_K_AUX, [&] {
+              if (max_ngrp <= 64 && !(c0->diag & kDiagSerialTop)) {
+                klaunch(c0, k_group_top_multi<T, RNG, SP>, dim3((unsigned)max_ngrp, (unsigned)na), dim3(64), 0, dd, na,
+                        cst, gen, iter);
+              } else {
+                klaunch(c0, k_group_multi<T, SP>, dim3((unsigned)max_ngrp, (unsigned)na), dim3(64), 0, dd, na, cst, gen);
+                if (wide)
+                  klaunch(c0, k_top_wide_multi<T, RNG, SP>, dim3((unsigned)na), dim3(64 * kTopWaves), glds, dd, na, cst,
+                          gen, iter);
+                else
+                  klaunch(c0, k_top_multi<T, RNG, SP>, dim3((unsigned)na), dim3(64), 0, dd, na, cst, gen, iter);
+              }
+            }));
+            continue;
+          }
+        }
         RET(launch_ext(c0, PFMPE_K_PROPAGATE, [&] {
           if (c0->prune)
             klaunch(c0, k_propagate_weigh_multi<T, RNG, MAXM, true, SP>, dim3((unsigned)total), dim3(kBlock), lds_w, dd,
@@ -762,6 +846,7 @@ struct Seq {
                     dd, db, na, (const uint32_t*)dstat, gen, iter);
         }));
       }
+      for (int i = 0; i < na; ++i) cs[act[i]]->last_weigh_pass = pk ? PFMPE_WEIGH_PK : PFMPE_WEIGH_BLOCKS;
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
         if (all_kept)
           klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
@@ -810,6 +895,7 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in);
 
 template <typename T, int RNG, typename SP>
 int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* table, size_t tbytes, const GridHdr& gh) {
+  c->frame_owner_out = -1;  // one-launch frames materialise the new prior (finish() may set it)
   FrameArgsT<T> fa = build_args<T>(c, in);
   fa.tbytes = (int32_t)tbytes;
   fa.grid = grid_args<T>(gh, fa.B, (float)fa.tolq);
@@ -885,6 +971,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   bool all5 = true;  // every stream has exactly kExactM markers: the exact 5-slot bucket serves the batch
   for (int s = 0; s < S; ++s) {
     pfmpe_ctx* c = cs[s];
+    c->frame_owner_out = -1;  // batches materialise every stream's new prior
     all5 = all5 && c->M == kExactM;
     fas[s] = build_args<T>(c, &in[s]);
     for (int q = 0; q < 12; ++q) {
@@ -1066,6 +1153,8 @@ FrameArgsT<T> build_args(const pfmpe_ctx* c, const pfmpe_frame_in* in) {
   fa.diag = c->diag;
   fa.wait_ticks = (uint32_t)std::min<int64_t>(c->wait_bound_us * 100, 0xffffffffll);  // s_memrealtime: 100 MHz
   fa.ld = c->ld;
+  fa.owner = prior_owner_ptr(c);
+  fa.owner_out = nullptr;
   return fa;
 }
 

@@ -64,7 +64,7 @@ void launch_export(pfmpe_ctx* c, int N, const double* anchor) {
   Pose12<T> a;
   for (int q = 0; q < 12; ++q) a.v[q] = (T)anchor[q];
   hipLaunchKernelGGL((k_export<T, SP>), dim3((N + 255) / 256), dim3(256), 0, c->stream,
-                     (const SP*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld, a);
+                     (const SP*)c->d_state[c->prior_idx], c->d_xfer, N, c->ld, a, prior_owner_ptr(c));
 }
 
 
@@ -150,6 +150,15 @@ void take_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   c->last_kept_slot = o.kept_slot;
   c->last_kept_iter = o.kept_iter;
   if (o.resampled) {  // newPoseEstimation = resampled set (PE:681, 727), anchored at this frame's current pose
+    if (c->frame_owner_out >= 0 && o.kept_slot >= 0 && o.kept_slot < 2 && c->d_prop[o.kept_slot]) {
+      // deferred resampling: the kept buffer is the new prior's storage (read through the owner indices k_resample
+      // wrote); the unused post buffer becomes that weight slot's kept buffer for the next frame
+      std::swap(c->d_prop[o.kept_slot], c->d_state[1 - c->prior_idx]);
+      c->prior_owner = c->frame_owner_out;
+    } else {
+      c->prior_owner = -1;
+    }
+    c->frame_owner_out = -1;
     c->prior_idx = 1 - c->prior_idx;
     std::memcpy(c->anchor[c->prior_idx], in->current_pose, 12 * sizeof(double));
   }
@@ -331,6 +340,9 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
     case PFMPE_OPT_KEEP_PROPAGATED:
       c->keep_prop = value != 0;
       return PFMPE_OK;
+    case PFMPE_OPT_DEFER_RESAMPLE:
+      c->defer = value != 0;
+      return PFMPE_OK;
     case PFMPE_OPT_MULTI_MAX_BLOCKS:
       if (value < 1 || value > kMultiMaxBlocks) return fail(c, PFMPE_E_ARG, "set_option: MULTI_MAX_BLOCKS is 1 .. 160000");
       c->multi_max_blocks = value;
@@ -368,6 +380,7 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
   HIPCHK(c, hipMemcpyAsync(c->d_xfer, poses, (size_t)N * 12 * sizeof(double), hipMemcpyHostToDevice, c->stream));
   // fp16 state: the set's anchor is its first particle (deltas of a concentrated set stay small)
   std::memcpy(c->anchor[c->prior_idx], poses, 12 * sizeof(double));
+  c->prior_owner = -1;  // stored in particle order
   if (c->state_dtype == PFMPE_STATE_F64)
     launch_import<double, double>(c, N, c->anchor[c->prior_idx]);
   else if (c->state_dtype == PFMPE_STATE_F16)
@@ -566,6 +579,7 @@ int pfmpe_predict_roi(pfmpe_ctx* c, const pfmpe_roi_in* in, pfmpe_roi_out* out) 
   ra.N = N;
   ra.M = c->M;
   ra.ld = c->ld;
+  ra.owner = prior_owner_ptr(c);
   double* part = c->d_roi + 4;
   RET(launch(c, PFMPE_K_ROI, [&] {
     const void* st = c->d_state[c->prior_idx];

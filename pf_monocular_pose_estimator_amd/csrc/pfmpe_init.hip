@@ -375,7 +375,7 @@ void export1(pfmpe_ctx* c) {
   Pose12<T> a;
   for (int q = 0; q < 12; ++q) a.v[q] = (T)c->anchor[c->prior_idx][q];
   hipLaunchKernelGGL((k_export<T, SP>), dim3(1), dim3(64), 0, c->stream, (const SP*)c->d_state[c->prior_idx],
-                     c->d_xfer, 1, c->ld, a);
+                     c->d_xfer, 1, c->ld, a, prior_owner_ptr(c));
 }
 // slot 0 of the resident set -> d_xfer[0..11]
 int export_slot0(pfmpe_ctx* c) {
@@ -400,6 +400,7 @@ void import_n(pfmpe_ctx* c, int N, int slot) {
 int import_xfer(pfmpe_ctx* c, int N, const double* anchor) {
   const int slot = c->prior_idx;
   std::memcpy(c->anchor[slot], anchor, 12 * sizeof(double));
+  c->prior_owner = -1;  // stored in particle order
   if (c->state_dtype == PFMPE_STATE_F64)
     import_n<double, double>(c, N, slot);
   else if (c->state_dtype == PFMPE_STATE_F16)

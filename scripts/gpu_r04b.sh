@@ -1,15 +1,18 @@
 #!/bin/bash
-# Round 4, k_weigh_pk first pass: bit-identity tests of the packed pass against k_weigh_stream, the parity tests
-# that run C4/C5-size frames through it, an A/B of C4 / C5 with and without it (PFMPE_DIAG 4096 = no pk), one
-# SQ_INSTS_VALU pass of each at C4.  Logs under gpurun_out/.
+# Round 4, k_weigh_pk + deferred resampling first pass: bit-identity tests of the packed pass against
+# k_weigh_stream, the batched tests (incl. the corrupt-descriptor report and the streaming packed batch), exact
+# resample counts at C2-C5 sizes, the parity and frame-shape suites (deferred priors through every consumer);
+# then an A/B of C4 / C5: default (pk + deferral), PFMPE_DIAG 16384 (no deferral), 4096|16384 (round-3 path);
+# one SQ_INSTS_VALU pass of each weighing kernel at C4.  Logs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gpu_weigh_pk.py tests/test_gpu_resample_counts.py -x -v \
+timeout -k 10 1000 python -u -m pytest tests/test_gpu_weigh_pk.py tests/test_gpu_multi.py tests/test_gpu_resample_counts.py \
+  tests/test_gpu_parity.py tests/test_gpu_frame_shapes.py -x -v \
   --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r04b_tests.log 2>&1; r=$?
-grep -E "PASS|FAIL|ERROR|passed|failed|Error|assert" gpurun_out/r04b_tests.log | tail -25
+grep -E "PASS|FAIL|ERROR|passed|failed|Error|assert" gpurun_out/r04b_tests.log | tail -40
 [ $r -eq 0 ] || exit $r
 for rep in 1 2; do
 for c in C4 C5; do
-  for d in 0 4096; do
+  for d in 0 16384 20480; do
     timeout -k 10 300 python -u bench.py --config $c --steps 100 --warmup 10 --cpu-frames 0 --worst-frames 0 \
       --scale-ref-steps 0 --exact-steps 0 --multi-sweep none --diag $d > gpurun_out/r04b_bench_${c}_$d.log 2>&1 \
       || { tail -5 gpurun_out/r04b_bench_${c}_$d.log; exit 1; }
@@ -19,7 +22,7 @@ print('$c diag=$d', round(d['ms_per_step']*1e3,1), 'us/frame', round(d['value']/
   done
 done
 done
-for d in 0 4096; do
+for d in 0 20480; do
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     --output-format csv -d gpurun_out/r04b_pmc_$d -o run -- python3 bench.py --config C4 --steps 20 --warmup 3 \
     --cpu-frames 0 --no-timing --worst-frames 0 --scale-ref-steps 0 --exact-steps 0 --multi-sweep none --diag $d \
@@ -27,7 +30,7 @@ for d in 0 4096; do
 done
 python3 - <<'PY'
 import csv, glob, collections
-for d in (0, 4096):
+for d in (0, 20480):
     f = glob.glob(f"gpurun_out/r04b_pmc_{d}/**/*counter_collection.csv", recursive=True)
     if not f: print("no csv", d); continue
     acc = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
@@ -36,7 +39,6 @@ for d in (0, 4096):
         acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
         n[(k, row["Counter_Name"])] += 1
     for k, c in acc.items():
-        if "weigh" not in k: continue
         cnt = n[(k, "SQ_WAVES")] or 1
         w = c["SQ_WAVES"]
         print(d, k, "launches", cnt, "VALU/wave", round(c["SQ_INSTS_VALU"] / max(w, 1), 1), "SALU/wave",

@@ -88,9 +88,9 @@ def _same(a, b, tag):
             assert np.array_equal(a[k], b[k]), (tag, k)
 
 
-def _check_batch(state, rng, n_frames, cfgs=STREAMS, strict_occlude=True):
+def _check_batch(state, rng, n_frames, cfgs=STREAMS, strict_occlude=True, passes_out=None):
     streams = _streams(n_frames, cfgs)
-    batch, solo, occl_iters = [], [], []
+    batch, solo, occl_iters, passes = [], [], [], []
     for (st, frames, how), (N, M, *_rest) in zip(streams, cfgs):
         pair = []
         for fused in (2, 0):  # the solo engine takes its default shape; the batch always runs two launches
@@ -117,9 +117,12 @@ def _check_batch(state, rng, n_frames, cfgs=STREAMS, strict_occlude=True):
                 if how == "empty":
                     assert outs[s].flag_fail == pf.FLAG_REINIT
             assert batch[0].info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+            passes.append(batch[0].info(pf.INFO_LAST_WEIGH_PASS))
     finally:
         for e in batch + solo:
             e.close()
+    if passes_out is not None:
+        passes_out.extend(passes)
     return occl_iters
 
 
@@ -389,3 +392,16 @@ def test_multi_corrupt_descriptor_is_reported(state, rng):
     finally:
         for e in batch + solo:
             e.close()
+
+
+@pytest.mark.parametrize("state", [pf.STATE_F32, pf.STATE_F16])
+def test_multi_streaming_pk_batch_equals_single_streams(state):
+    """The streaming packed batch (k_weigh_pk_multi + the batched group / top hand-off; every stream 5 LEDs with
+    B >= M, fp32 or fp16, Philox): per-stream workgroup shares of different sizes, one occluded stream (all 80
+    iterations: later rounds run a subset), one stream beyond one tile of groups (3M particles: 108 groups, the
+    k_group_multi + k_top_wide_multi hand-off), N not a multiple of 128.  Every stream bit-identical to its own
+    pfmpe_step (whose two-launch frames run k_weigh_pk), over 3 frames."""
+    cfgs = [(100_000, 5, 50, False, ""), (4099, 5, 50, False, "occlude"), (3_000_017, 5, 50, False, ""),
+            (777, 5, 20, False, "")]
+    _check_batch(state, pf.RNG_PHILOX, 3, cfgs, passes_out=(passes := []))
+    assert passes and all(p == pf.WEIGH_PK for p in passes), passes
