@@ -350,27 +350,19 @@ __device__ __forceinline__ void buf_st(__half v, __amdgpu_buffer_rsrc_t r, uint3
 // access per lane (6 instead of 12 VMEM instructions per particle, 256 B per wave instruction), and the pair is
 // the register layout the kernels already use (RawState<__half>, store_state_words_f16).  0 keeps 12 planes of
 // halves (A/B).  fp32 / fp64 planes are unchanged.
-// fp32 state likewise (PFMPE_F32_PAIRS): 6 planes of 64-bit pairs, one dwordx2 per lane and pair.  Default 0:
-// measured C5 k_resample -2 us but C3 k_propagate_weigh +1..5 us, and the one batched run that faulted this
-// round (an aperture violation in k_resample_multi, 16 C2 streams as two concurrent batches) used it
-// (profiles/r03/multi_fault_f32pairs_abm_new.log); not kept until that is explained.
+// fp32 state keeps 12 plain planes.  Round 3 also tried 6 planes of 64-bit pairs (PFMPE_F32_PAIRS): -2 us on C5's
+// k_resample, +1..5 us on C3's weighing; round 4 removed it: deferred resampling (k_resample writes owner indices,
+// no state planes) took away the only kernel it helped.
 #ifndef PFMPE_F16_PAIRS
 #define PFMPE_F16_PAIRS 1
-#endif
-#ifndef PFMPE_F32_PAIRS
-#define PFMPE_F32_PAIRS 0
 #endif
 template <typename SP>
 __host__ __device__ __forceinline__ constexpr bool f16_pairs() {
   return std::is_same<SP, __half>::value && PFMPE_F16_PAIRS != 0;
 }
 template <typename SP>
-__host__ __device__ __forceinline__ constexpr bool f32_pairs() {
-  return std::is_same<SP, float>::value && PFMPE_F32_PAIRS != 0;
-}
-template <typename SP>
 __host__ __device__ __forceinline__ int64_t plane_index(int q, int64_t n, int64_t ld) {
-  if constexpr (f16_pairs<SP>() || f32_pairs<SP>())
+  if constexpr (f16_pairs<SP>())
     return (int64_t)(q >> 1) * 2 * ld + 2 * n + (q & 1);
   else
     return (int64_t)q * ld + n;
@@ -387,15 +379,6 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
       const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)p * pps, 0);
       v[2 * p] = __ushort_as_half((unsigned short)(w & 0xffffu));
       v[2 * p + 1] = __ushort_as_half((unsigned short)(w >> 16));
-    }
-  } else if constexpr (f32_pairs<SP>()) {
-    const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
-    const uint32_t pps = (uint32_t)(ld * 8);
-#pragma unroll
-    for (int p = 0; p < 6; ++p) {
-      const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)n * 8u, (uint32_t)p * pps, 0);
-      v[2 * p] = __uint_as_float(w[0]);
-      v[2 * p + 1] = __uint_as_float(w[1]);
     }
   } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
@@ -418,14 +401,6 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
       const uint32_t w = (uint32_t)__half_as_ushort(v[2 * p]) | ((uint32_t)__half_as_ushort(v[2 * p + 1]) << 16);
       __builtin_amdgcn_raw_buffer_store_b32(w, r, (uint32_t)k * 4u, (uint32_t)p * pps, 0);
     }
-  } else if constexpr (f32_pairs<SP>()) {
-    const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
-    const uint32_t pps = (uint32_t)(ld * 8);
-    typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int p = 0; p < 6; ++p)
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2v{__float_as_uint(v[2 * p]), __float_as_uint(v[2 * p + 1])}, r,
-                                            (uint32_t)k * 8u, (uint32_t)p * pps, 0);
   } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
@@ -504,13 +479,6 @@ __device__ __forceinline__ void load_state_prefetch(const SP* __restrict__ base,
         x.x = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k) * ps, 0);
         x.y = __builtin_amdgcn_raw_buffer_load_b16(r, (uint32_t)n * 2u, (uint32_t)(2 * k + 1) * ps, 0);
         R.p[k] = x;
-      }
-    } else if constexpr (f32_pairs<SP>()) {  // one dwordx2 per pair plane
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const auto w = __builtin_amdgcn_raw_buffer_load_b64(r, (uint32_t)n * 8u, (uint32_t)k * (uint32_t)(ld * 8), 0);
-        R.v[2 * k] = w[0];
-        R.v[2 * k + 1] = w[1];
       }
     } else {
 #pragma unroll

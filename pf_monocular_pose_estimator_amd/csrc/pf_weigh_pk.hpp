@@ -170,7 +170,6 @@ __device__ __forceinline__ void store_kept(SP* __restrict__ dst, int64_t ld, int
     }
   } else {
     (void)D;
-    static_assert(PFMPE_F32_PAIRS == 0, "k_weigh_pk stores fp32 planes");
     const uint32_t ps = (uint32_t)(ld * 4);
 #pragma unroll
     for (int q = 0; q < 12; ++q)
