@@ -81,6 +81,10 @@ def parse():
                     help="frames of the fp64 / reference-RNG (parity mode) C2 point beside the default line (0 = skip)")
     ap.add_argument("--scale-ref-steps", type=int, default=100,
                     help="frames of the one-GPU C5 reference beside the default C2 line (0 = skip)")
+    ap.add_argument("--single-points", default="C3,C4",
+                    help="configs timed as one stream beside the default C2 line, with their per-kernel HIP-event "
+                         "averages (comma list; 'none' skips)")
+    ap.add_argument("--single-steps", type=int, default=100, help="timed frames per --single-points config")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
     return ap.parse_args()
@@ -311,9 +315,10 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
 
 
 def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args,
-                        state_dtype=None):
+                        state_dtype=None, kernels=False):
     """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
-    every frame blocks on its record)."""
+    every frame blocks on its record).  kernels: also bracket the kernels of every 10th timed frame with HIP
+    events and report their averages, the frame shape and the weighing pass."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
     st = syn.make_stream(cfg, warmup + steps)
     eng = pf.Engine(device=device, max_particles=cfg.N,
@@ -333,11 +338,25 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
                                  dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index) for f in st.frames]
         for f in frames[:warmup]:
             eng.step(f)
+        if kernels:
+            eng.reset_kernel_stats()
+            eng.set_option(pf.OPT_TIMING, max(1, steps // 10))
         t0 = time.perf_counter()
         outs = eng.step_batch(frames[warmup:])
         el = time.perf_counter() - t0
-        return {"value": sum(cfg.N * o.iters for o in outs) / el, "unit": "particle-updates/s",
-                "ms_per_frame": el * 1e3 / steps, "frames": steps}
+        pt = {"value": sum(cfg.N * o.iters for o in outs) / el, "unit": "particle-updates/s",
+              "ms_per_frame": el * 1e3 / steps, "frames": steps,
+              "iters_per_frame": float(np.mean([o.iters for o in outs]))}
+        if kernels:
+            eng.set_option(pf.OPT_TIMING, 0)
+            stats = eng.kernel_stats()
+            pt["frame_shape"] = {0: "two-launch", 1: "k_frame", 2: "k_frame2"}.get(eng.info(pf.INFO_LAST_SHAPE))
+            wname = {pf.WEIGH_STREAM: "k_weigh_stream", pf.WEIGH_PK: "k_weigh_pk"}.get(
+                eng.info(pf.INFO_LAST_WEIGH_PASS), "k_propagate_weigh")
+            pt["weigh_pass"] = wname
+            pt["per_kernel_avg_us"] = {(wname if k == "k_propagate_weigh" else k): round(v[1] * 1e3 / v[0], 3)
+                                       for k, v in stats.items() if v[0] > 0}
+        return pt
     finally:
         eng.close()
 
@@ -478,6 +497,20 @@ def main():
         scale_ref["what"] = ("one C5 stream (BASELINE.json configs[4]: M=5, B=50, N=1M, f32) on this GPU, timed like "
                              "the main line: the per-GPU workload of bench.py --gpus N > 1, for its N = 1 point")
 
+    singles = None
+    if default_line and rank == 0 and args.single_points not in ("", "none") and args.single_steps > 0:
+        # the heavy single-stream configs (BASELINE.json configs[2] / [3]) timed like the main line, each with its
+        # own per-kernel HIP-event averages (untimed by the driver's contract)
+        singles = {}
+        for name in [x for x in args.single_points.split(",") if x]:
+            st_ = pf.STATE_F16 if name == "C4" else pf.STATE_F32
+            pt = single_stream_point(pf, syn, syn.CONFIGS[name], args.single_steps, 10, prm.rng_mode, device, sid,
+                                     args, state_dtype=st_, kernels=True)
+            pt["state"] = "f16" if st_ == pf.STATE_F16 else "f32"
+            Sb = 24 if st_ == pf.STATE_F16 else 48
+            pt["frame_frac"] = round(pt["value"] * (3 * Sb + 8) / 1e9 / HBM_PEAK_GBPS, 4)
+            singles[name] = pt
+
     if rank == 0:
         S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
         k_mean = float(np.mean(iters)) if iters else 1.0
@@ -486,9 +519,10 @@ def main():
         timed = {k: v for k, v in stats.items() if v[0] > 0}
         if shape == pf.SHAPE_FRAME2 and "k_frame" in timed:  # PFMPE_K_FRAME times whichever one-launch kernel ran
             timed["k_frame2"] = timed.pop("k_frame")
-        if weigh_pass == pf.WEIGH_STREAM and "k_propagate_weigh" in timed:  # the streaming weighing pass
-            timed["k_weigh_stream"] = timed.pop("k_propagate_weigh")
-            ab["k_weigh_stream"] = ab["k_propagate_weigh"]
+        wname = {pf.WEIGH_STREAM: "k_weigh_stream", pf.WEIGH_PK: "k_weigh_pk"}.get(weigh_pass)
+        if wname and "k_propagate_weigh" in timed:  # the streaming / packed weighing passes
+            timed[wname] = timed.pop("k_propagate_weigh")
+            ab[wname] = ab["k_propagate_weigh"]
         if timed:
             dom = max(timed, key=lambda k: timed[k][1])
             launches, ms = timed[dom]
@@ -543,6 +577,7 @@ def main():
             "worst_case": worst,
             "multi_stream": multi,
             "scaling_reference": scale_ref,
+            "single_stream": singles,
             "parity_mode": exact,
         }
         print(json.dumps(line), flush=True)
