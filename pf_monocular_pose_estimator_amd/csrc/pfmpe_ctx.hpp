@@ -733,12 +733,20 @@ struct Seq {
         x.tcount_w = c->d_counters + c->max_grp;
         x.gcount_r = c->d_counters + c->max_grp + 1;
         x.tcount_r = c->d_counters + 2 * c->max_grp + 1;
-        // the stored set pays in batches only for fp16 state (round-3 A/B, DESIGN.md §4.2: 8 x C5 batches 5-8 %
-        // faster regenerating, 32 x C2 even); the choice changes no result
-        const bool kept = c->keep_prop && c->d_prop[0] && std::is_same<SP, __half>::value;
+        // The stored set with deferred resampling (k_resample_multi writes owner indices; the kept buffer becomes the
+        // stream's prior at take_step, as in finish()) for every state type; without deferral it pays in batches only
+        // for fp16 state (round-3 A/B, DESIGN.md §4.2: 8 x C5 batches 5-8 % faster regenerating).  No choice here
+        // changes a result.
+        const bool defer = c->defer && c->d_owner[0] && !(c->diag & kDiagNoDefer);
+        const bool kept = c->keep_prop && c->d_prop[0] && (defer || std::is_same<SP, __half>::value);
         x.prop0 = kept ? (SP*)c->d_prop[0] : nullptr;
         x.prop1 = kept ? (SP*)c->d_prop[1] : nullptr;
         all_kept = all_kept && kept;
+        c->frame_owner_out = -1;
+        if (kept && defer) {
+          c->frame_owner_out = c->prior_owner == 0 ? 1 : 0;
+          x.fa.owner_out = c->d_owner[c->frame_owner_out];
+        }
         x.cpart = c->d_cpart;
         x.cgroup = c->d_cgroup;
         x.counts = c->record_counts ? c->d_counts : nullptr;
@@ -971,7 +979,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   bool all5 = true;  // every stream has exactly kExactM markers: the exact 5-slot bucket serves the batch
   for (int s = 0; s < S; ++s) {
     pfmpe_ctx* c = cs[s];
-    c->frame_owner_out = -1;  // batches materialise every stream's new prior
+    c->frame_owner_out = -1;  // step_multi sets it for the streams it defers
     all5 = all5 && c->M == kExactM;
     fas[s] = build_args<T>(c, &in[s]);
     for (int q = 0; q < 12; ++q) {
