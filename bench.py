@@ -236,7 +236,7 @@ def occluded_frames(eng, st, rank: int, n: int, first_index: int):
 
 
 def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dtype: int, rng: int, device: int,
-                       sid0: int, prune: int, keep_prop: int, groups: int = 1):
+                       sid0: int, prune: int, keep_prop: int, groups: int = 1, diag: int = 0):
     """S independent streams of `base` on one GPU, each frame of all S run as ONE batch (pfmpe_step_multi:
     one weighing launch over every stream's blocks, one resampling launch, one finishing launch).  Blob tables
     come from each stream's staged bank; the timed loop is pfmpe_step_multi_batch (the C loop a tracker runs).
@@ -259,6 +259,8 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
             eng.set_option(pf.OPT_PRUNE, prune)
             if keep_prop >= 0:
                 eng.set_option(pf.OPT_KEEP_PROPAGATED, keep_prop)
+            if diag:
+                eng.set_option(99, diag)
             eng.stage_blob_bank([f.blobs for f in st.frames])
             engs.append(eng)
             frames.append([eng.make_frame(f.current_pose, f.predicted_pose, f.prediction, B=len(f.blobs),
@@ -473,7 +475,7 @@ def main():
         for cfg_, st_, Sb_, S_, G_ in plan:
             steps_ = args.multi_steps if cfg_.N <= 1_000_000 else max(10, args.multi_steps // 3)
             pt = multi_stream_point(pf, syn, cfg_, S_, steps_, 5, st_, prm.rng_mode, device, sid, args.prune,
-                                    args.keep_prop, G_)
+                                    args.keep_prop, G_, args.diag)
             pt["config"] = cfg_.name
             pt["state"] = {pf.STATE_F32: "f32", pf.STATE_F16: "f16", pf.STATE_F64: "f64"}[st_]
             pt["frac"] = round(pt["updates_per_s"] * (3 * Sb_ + 8) / 1e9 / HBM_PEAK_GBPS, 4)

@@ -45,3 +45,17 @@ for d in (0, 20480):
               round(c["SQ_INSTS_SALU"] / max(w, 1), 1), "LDS/wave", round(c["SQ_INSTS_LDS"] / max(w, 1), 1),
               "waves/launch", w / cnt, "VALU per 64 particles", round(c["SQ_INSTS_VALU"] / cnt / (1e7 / 64), 1))
 PY
+# batched A/B: 32 x C5 (two concurrent batches) and 2 x C4 (one batch), default (packed batch pass + deferral) vs
+# PFMPE_DIAG 16384 (no deferral: fp32 batches regenerate, fp16 batches materialise)
+for d in 0 16384; do
+  timeout -k 10 300 python -u bench.py --config C5 --steps 20 --warmup 5 --cpu-frames 0 --worst-frames 0 \
+    --scale-ref-steps 0 --exact-steps 0 --multi-sweep 32 --multi-groups 2 --multi-steps 30 --diag $d \
+    > gpurun_out/r04b_multi_C5_$d.log 2>&1 || { tail -5 gpurun_out/r04b_multi_C5_$d.log; exit 1; }
+  timeout -k 10 300 python -u bench.py --config C4 --steps 20 --warmup 5 --cpu-frames 0 --worst-frames 0 \
+    --scale-ref-steps 0 --exact-steps 0 --multi-sweep 2 --multi-groups 1 --multi-steps 30 --diag $d \
+    > gpurun_out/r04b_multi_C4_$d.log 2>&1 || { tail -5 gpurun_out/r04b_multi_C4_$d.log; exit 1; }
+  for c in C5 C4; do python3 -c "
+import json; d=json.loads(open('gpurun_out/r04b_multi_${c}_$d.log').read().strip().splitlines()[-1])
+print('$c diag=$d single', round(d['ms_per_step']*1e3,1), 'us', round(d['value']/1e9,2), 'G/s |',
+      [(p['streams'], p['groups'], round(p['updates_per_s']/1e9,2), p['frac']) for p in d['multi_stream']['points']])"; done
+done
