@@ -3275,10 +3275,18 @@ __device__ __forceinline__ void resample_phase(
     }
     if (blk != 0) return;
     if (!flat_wait(flat + kFlatCountSet, fa.flat_base_c + (uint32_t)fa.nblk, fa.wait_ticks)) return;  // abandoned
+    // every count partial of the frame (nblk <= kFlatMaxGroups * kGroup = 8 per lane) requested in ONE round
+    // trip, then combined; a lane past nblk holds the identity (count -1)
     int bv = -1, bi = 0x7fffffff;
-    for (int t = lane; t < fa.nblk; t += 64) {
-      const uint64_t cp = ld_wt(cpart + t);
-      cmb_max(bv, bi, lo32(cp), hi32(cp));
+    {
+      uint64_t cp[kFlatMaxGroups];
+#pragma unroll
+      for (int j = 0; j < kFlatMaxGroups; ++j) {
+        const int t = lane + 64 * j;
+        cp[j] = t < fa.nblk ? ld_wt(cpart + t) : pack2(-1, 0x7fffffff);
+      }
+#pragma unroll
+      for (int j = 0; j < kFlatMaxGroups; ++j) cmb_max(bv, bi, lo32(cp[j]), hi32(cp[j]));
     }
     wave_argmax(bv, bi);
     if (stamps && lane == 0) stamps[6] = rt_now();
