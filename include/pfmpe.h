@@ -346,7 +346,9 @@ enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 aft
        PFMPE_INFO_LAST_SHAPE = 3,       /* PFMPE_SHAPE_* of the last step (-1 before the first)      */
        PFMPE_INFO_GUARD_SKIPS = 4,      /* frames run as two launches because another was in flight  */
        PFMPE_INFO_N = 5,                /* current particle count                                    */
-       PFMPE_INFO_LAST_WEIGH_PASS = 6 };/* PFMPE_WEIGH_* of the last two-launch weighing (-1: none)  */
+       PFMPE_INFO_LAST_WEIGH_PASS = 6,  /* PFMPE_WEIGH_* of the last two-launch weighing (-1: none)  */
+       PFMPE_INFO_LAST_GRID = 7 };      /* 1: the last frame's blob table searched its cell grid; 0: the
+                                         * x-buckets (no grid for this table or its window; fp64)    */
 /* The two-launch shape's weighing pass: one block per 256 particles (k_propagate_weigh), or
  * resident blocks streaming over them with the next block's state prefetched (k_weigh_stream + k_group +
  * k_top), or the streaming pass with two particles per lane in packed fp32 (k_weigh_pk: 5 markers, fp32 / fp16

@@ -28,6 +28,7 @@ DIAG_NO_PK, DIAG_CORRUPT_DESC, DIAG_NO_DEFER = 4096, 8192, 16384
 OPT_DEFER_RESAMPLE = 9
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
 INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N, INFO_LAST_WEIGH_PASS = 1, 2, 3, 4, 5, 6
+INFO_LAST_GRID = 7
 WEIGH_BLOCKS, WEIGH_STREAM, WEIGH_PK = 0, 1, 2
 K_PROPAGATE, K_RESAMPLE, K_AUX, K_FRAME, K_ROI, K_FINAL, K_P3P_HIST, K_P3P_CHECK, K_DETECT, K_COUNT = range(10)
 

@@ -114,6 +114,10 @@ struct pfmpe_ctx {
   std::vector<size_t> bank_off;      // byte offset of frame f's table
   std::vector<int32_t> bank_B;
   std::vector<GridHdr> bank_grid;    // frame f's table grid header (host copy, for the kernel arguments)
+  std::vector<double> bank_blobs;    // the staged blobs and per-frame offsets, kept to rebuild the tables when
+  std::vector<int32_t> bank_offsets; // set_params changes tol_PF (the grid's window depends on it)
+  double bank_tol_pf = 0.0;          // the tol_PF the bank's tables were built for
+  int last_grid = -1;                // PFMPE_INFO_LAST_GRID
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
@@ -907,6 +911,7 @@ int dispatch_m(pfmpe_ctx* c, const pfmpe_frame_in* in, const unsigned char* tabl
   FrameArgsT<T> fa = build_args<T>(c, in);
   fa.tbytes = (int32_t)tbytes;
   fa.grid = grid_args<T>(gh, fa.B, (float)fa.tolq);
+  c->last_grid = fa.grid.on;
   for (int q = 0; q < 12; ++q) {  // fp16 state: anchors of the prior and of the new prior (current pose)
     fa.anc_in[q] = (T)c->anchor[c->prior_idx][q];
     fa.anc_out[q] = (T)in->current_pose[q];
@@ -998,6 +1003,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
       fas[s].tbytes = (int32_t)(c->bank_off[f + 1] - c->bank_off[f]);
       fas[s].grid = grid_args<T>(c->bank_grid[f], in[s].B, (float)fas[s].tolq);
     }
+    c->last_grid = fas[s].grid.on;
     total += fas[s].nblk;
     maxM = std::max(maxM, c->M);
   }

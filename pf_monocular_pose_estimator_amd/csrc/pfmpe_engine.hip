@@ -301,13 +301,20 @@ int pfmpe_set_model(pfmpe_ctx* c, const double* markers_xyz, int M, const double
   return PFMPE_OK;
 }
 
+static int build_bank(pfmpe_ctx* c);
+
 int pfmpe_set_params(pfmpe_ctx* c, const pfmpe_params* p) {
   if (!c || !p) return PFMPE_E_ARG;
   if (!(p->tol > 0) || !(p->tol_pf >= 0) || p->max_iter < 1 || p->max_iter > kMaxIter || p->exit_cap < 0 ||
       p->accept_cap < 0 ||
       (p->rng_mode != PFMPE_RNG_REFERENCE && p->rng_mode != PFMPE_RNG_PHILOX))
     return fail(c, PFMPE_E_ARG, "set_params: invalid parameter");
+  const bool retable = c->d_bank && p->tol_pf != c->bank_tol_pf;
   c->params = *p;
+  if (retable) {  // the staged bank's grids were built for another tol_PF
+    RET(set_device(c));
+    return build_bank(c);
+  }
   return PFMPE_OK;
 }
 
@@ -397,6 +404,35 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
   return PFMPE_OK;
 }
 
+// (Re)builds the device bank from c->bank_blobs / bank_offsets with the parameters current now.  The table of a
+// frame carries a grid whose window is tol_PF's: set_params rebuilds the bank when tol_PF changes, so a bank
+// staged before set_params (or a later change) never leaves the frames on the slower x-bucket path
+// (ADVICE r03).
+static int build_bank(pfmpe_ctx* c) {
+  const int nframes = (int)c->bank_offsets.size() - 1;
+  if (c->d_bank) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(c->d_bank));
+    c->d_bank = nullptr;
+  }
+  c->bank_off.assign(nframes + 1, 0);
+  c->bank_B.assign(nframes, 0);
+  c->bank_grid.assign(nframes, GridHdr{});
+  std::vector<unsigned char> host, one(table_max_bytes(c));
+  for (int f = 0; f < nframes; ++f) {
+    c->bank_B[f] = c->bank_offsets[f + 1] - c->bank_offsets[f];
+    const size_t n = build_table(c, c->bank_blobs.data() + 2 * (size_t)c->bank_offsets[f], c->bank_B[f], one.data());
+    host.insert(host.end(), one.begin(), one.begin() + n);
+    c->bank_off[f + 1] = c->bank_off[f] + n;
+    c->bank_grid[f] = *(const GridHdr*)(one.data() + grid_off(c, c->bank_B[f]));
+  }
+  HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
+  HIPCHK(c, hipMemcpyAsync(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // `host` goes out of scope; the frames read the bank in this stream
+  c->bank_tol_pf = c->params.tol_pf;
+  return PFMPE_OK;
+}
+
 int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offsets, int nframes) {
   if (!c) return PFMPE_E_ARG;
   if (!blobs || !offsets || nframes < 1) return fail(c, PFMPE_E_ARG, "stage_blob_bank: bad arguments");
@@ -406,28 +442,10 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
     if (B > c->max_blobs) return fail(c, PFMPE_E_CAP, "stage_blob_bank: frame exceeds max_blobs");
   }
   RET(set_device(c));
-  if (c->d_bank) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipFree(c->d_bank));
-    c->d_bank = nullptr;
-  }
-  c->bank_off.assign(nframes + 1, 0);
-  c->bank_B.assign(nframes, 0);
-  // tables are built with the parameters current now (their grid's window); a frame stepped later with a
-  // wider tol_PF falls back to the x-buckets of the same table (column_minima checks the grid's window)
-  c->bank_grid.assign(nframes, GridHdr{});
-  std::vector<unsigned char> host, one(table_max_bytes(c));
-  for (int f = 0; f < nframes; ++f) {
-    c->bank_B[f] = offsets[f + 1] - offsets[f];
-    const size_t n = build_table(c, blobs + 2 * (size_t)offsets[f], c->bank_B[f], one.data());
-    host.insert(host.end(), one.begin(), one.begin() + n);
-    c->bank_off[f + 1] = c->bank_off[f] + n;
-    c->bank_grid[f] = *(const GridHdr*)(one.data() + grid_off(c, c->bank_B[f]));
-  }
-  HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
-  HIPCHK(c, hipMemcpyAsync(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // `host` goes out of scope; the frames read the bank in this stream
-  return PFMPE_OK;
+  c->bank_offsets.assign(offsets, offsets + nframes + 1);
+  c->bank_blobs.assign(blobs + 2 * (size_t)offsets[0], blobs + 2 * (size_t)offsets[nframes]);
+  for (auto& o : c->bank_offsets) o -= offsets[0];
+  return build_bank(c);
 }
 
 int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
@@ -727,6 +745,7 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case PFMPE_INFO_FUSED_FALLBACKS: *value = c->fused_fallbacks; return PFMPE_OK;
     case PFMPE_INFO_LAST_SHAPE: *value = c->last_shape; return PFMPE_OK;
     case PFMPE_INFO_LAST_WEIGH_PASS: *value = c->last_weigh_pass; return PFMPE_OK;
+    case PFMPE_INFO_LAST_GRID: *value = c->last_grid; return PFMPE_OK;
     case PFMPE_INFO_GUARD_SKIPS: *value = c->guard_skips; return PFMPE_OK;
     case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
     default: return PFMPE_E_ARG;
