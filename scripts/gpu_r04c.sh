@@ -20,6 +20,8 @@ for rep in 1 2 3; do
   run drv_notiming_$rep --steps 20 --warmup 5 --no-timing || exit 1
   run drv_p10_$rep --steps 20 --warmup 5 --timing-period 10 || exit 1
   run long_$rep --steps 200 --warmup 20 || exit 1
+  HIP_FORCE_DEV_KERNARG=1 run devka_$rep --steps 20 --warmup 5 || exit 1
+  HIP_FORCE_DEV_KERNARG=0 run hostka_$rep --steps 20 --warmup 5 || exit 1
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04c_trace -o run -- \
   python3 bench.py --steps 20 --warmup 5 --cpu-frames 0 --worst-frames 0 --scale-ref-steps 0 --exact-steps 0 \
