@@ -6,7 +6,7 @@
 # one SQ_INSTS_VALU pass of each weighing kernel at C4.  Logs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests/test_gpu_weigh_pk.py tests/test_gpu_multi.py tests/test_gpu_resample_counts.py \
-  tests/test_gpu_defer.py tests/test_gpu_bank_retable.py tests/test_gpu_parity.py tests/test_gpu_frame_shapes.py -x -v \
+  tests/test_gpu_defer.py tests/test_gpu_bank_retable.py tests/test_gpu_grid_far.py tests/test_gpu_parity.py tests/test_gpu_frame_shapes.py -x -v \
   --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r04b_tests.log 2>&1; r=$?
 grep -E "PASS|FAIL|ERROR|passed|failed|Error|assert" gpurun_out/r04b_tests.log | tail -40
 [ $r -eq 0 ] || exit $r

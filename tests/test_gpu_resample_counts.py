@@ -40,13 +40,15 @@ def test_counts_match_exact_stratified_assignment(name):
     stats = []
     try:
         for f, fr in enumerate(st.frames):
-            blobs = fr.blobs
+            blobs, kw = fr.blobs, {}
             if f == 1:  # one LED's blob hidden: the exit rule never fires (PE:616), 80 iterations
                 uv0 = syn.project(st.K, fr.truth, st.markers)[0]
                 blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
+                if name == "C3":  # 12 LEDs among 200 heavy outliers: an outlier near LED 0 can still let the exit
+                    kw = {"force_iters": 80}  # rule fire, so the 80 iterations are forced (pfmpe_frame_in.force_iters)
             seed = 5151 + 7 * f
             out = eng.step(eng.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=blobs, dt=fr.dt,
-                                          seed=seed, frame_idx=f)).as_dict()
+                                          seed=seed, frame_idx=f, **kw)).as_dict()
             assert eng.info(pf.INFO_LAST_SHAPE) == shape
             assert out["accepted"] == 1 and out["resampled"] == 1
             if f == 1:
