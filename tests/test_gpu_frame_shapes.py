@@ -237,12 +237,16 @@ def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy, rng, prune):
     over a steady frame and an 80-iteration frame (one LED hidden), one tile of groups (140k) and several
     (1.2M: 4,688 blocks in 74 groups; 3M: 109 groups), fp64 / fp32 / fp16 state, both RNG streams, pruned and
     unpruned.  Beyond one tile of groups the streaming pass's top is k_top_wide (16 waves, the per-tile passes
-    in parallel); the one-block pass keeps propagate_top's serial tiles."""
+    in parallel); the one-block pass keeps propagate_top's serial tiles.  The packed pass (k_weigh_pk, taken by
+    default where it applies: fp32 compute, Philox, 5 markers) is a third variant of the same pass."""
     cfg = syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy)
     st = syn.make_stream(cfg, 2)
     prior = st.prior(fast=True)
     res = []
-    for diag in (pf.DIAG_FORCE_STREAM, pf.DIAG_NO_STREAM):
+    variants = [(pf.DIAG_FORCE_STREAM | pf.DIAG_NO_PK, (pf.WEIGH_STREAM,)),
+                (pf.DIAG_FORCE_STREAM, (pf.WEIGH_STREAM, pf.WEIGH_PK)),
+                (pf.DIAG_NO_STREAM, (pf.WEIGH_BLOCKS,))]
+    for diag, passes in variants:
         eng = make_engine(N, st.markers, st.K, state, rng, prune=prune, fused=0)
         eng.set_option(pf.OPT_DIAG, diag)
         eng.set_prior(prior)
@@ -262,15 +266,15 @@ def test_streaming_weighing_is_bit_identical(state, N, M, B, heavy, rng, prune):
                 snap["counts"] = eng.get_counts()
             snaps.append(snap)
         assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
-        assert eng.info(pf.INFO_LAST_WEIGH_PASS) == (pf.WEIGH_STREAM if diag == pf.DIAG_FORCE_STREAM
-                                                     else pf.WEIGH_BLOCKS)
+        assert eng.info(pf.INFO_LAST_WEIGH_PASS) in passes, (diag, eng.info(pf.INFO_LAST_WEIGH_PASS))
         eng.close()
         res.append(snaps)
     assert res[0][1]["out"]["iters"] == 80
-    for a, b in zip(*res):
-        for k, v in a["out"].items():
-            assert np.array_equal(np.asarray(v), np.asarray(b["out"][k])), k
-        for k in ("w", "p0", "p1", "counts"):
-            assert (k in a) == (k in b)
-            if k in a:
-                assert np.array_equal(a[k], b[k]), k
+    for other in res[:2]:
+        for a, b in zip(other, res[2]):
+            for k, v in a["out"].items():
+                assert np.array_equal(np.asarray(v), np.asarray(b["out"][k])), k
+            for k in ("w", "p0", "p1", "counts"):
+                assert (k in a) == (k in b)
+                if k in a:
+                    assert np.array_equal(a[k], b[k]), k
