@@ -132,24 +132,22 @@ __device__ __forceinline__ void draw_words(const U32x4& o, float* f) {
   f[5] = u21_bits(((o.z << 10) & 0x1FFC00u) | ((o.w & 0x3FFu) | 0x4B000000u));
 }
 
-// the state of the task's two particles, prefetched as raw words (fp16: the six pair-plane dwords; fp32: twelve)
+// 12 state values of both particles of the task as pairs {A, B} (fp16: plus the anchor), from the raw words
+// prefetched for each (fp16: the six pair-plane dwords; fp32: twelve).  Two separate RawState objects: held as
+// one aggregate {a, b}, the fp32 instance kept a's words in scratch across the loop (stored right after the
+// prefetch loads, which made the wave wait for them, and reloaded at the next task).
 template <typename SP>
-struct Raw2 {
-  RawState<SP> a, b;
-};
-// 12 state values of both particles as pairs {A, B} (fp16: plus the anchor)
-template <typename SP>
-__device__ __forceinline__ void decode2(const Raw2<SP>& R, const float* anc, f32x2* A) {
+__device__ __forceinline__ void decode2(const RawState<SP>& Ra, const RawState<SP>& Rb, const float* anc, f32x2* A) {
   if constexpr (std::is_same<SP, __half>::value) {
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const uint32_t wa = __builtin_bit_cast(uint32_t, R.a.p[k]), wb = __builtin_bit_cast(uint32_t, R.b.p[k]);
+      const uint32_t wa = __builtin_bit_cast(uint32_t, Ra.p[k]), wb = __builtin_bit_cast(uint32_t, Rb.p[k]);
       A[2 * k] = f32x2{f16_plus<0>(wa, anc[2 * k]), f16_plus<0>(wb, anc[2 * k])};
       A[2 * k + 1] = f32x2{f16_plus<1>(wa, anc[2 * k + 1]), f16_plus<1>(wb, anc[2 * k + 1])};
     }
   } else {
 #pragma unroll
-    for (int q = 0; q < 12; ++q) A[q] = f32x2{__uint_as_float(R.a.v[q]), __uint_as_float(R.b.v[q])};
+    for (int q = 0; q < 12; ++q) A[q] = f32x2{__uint_as_float(Ra.v[q]), __uint_as_float(Rb.v[q])};
   }
 }
 
@@ -289,6 +287,7 @@ __device__ __forceinline__ uint32_t sopaque(uint32_t x) {
 #define PFMPE_WEIGH_PK_MIN_WAVES 1
 #endif
 
+
 // The pass for one stream: workgroup wg of nwg resident workgroups (the one-stream kernel: blockIdx / gridDim; the
 // batched kernel: the stream's share of the grid).  fa_words: the frame arguments as words (kernarg segment or the
 // stream's descriptor) for the LDS constants.
@@ -322,11 +321,11 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
     ra = own ? (int)own[n] : n;
     rb = own ? (int)own[m] : m;
   };
-  Raw2<SP> R{};
+  RawState<SP> Ra{}, Rb{};
   int rA, rB;
   rows_of(tk, rA, rB);
-  load_state_prefetch<SP>(prior, fa.ld, rA, true, R.a);
-  load_state_prefetch<SP>(prior, fa.ld, rB, true, R.b);
+  load_state_prefetch<SP>(prior, fa.ld, rA, true, Ra);
+  load_state_prefetch<SP>(prior, fa.ld, rB, true, Rb);
   rows_of(tk + nwaves, rA, rB);
   stage_consts_from(fa_words, sc);
   if (threadIdx.x < 12) {
@@ -351,13 +350,13 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
     const int nA = tk * 128 + lane, nB = nA + 64;
     const bool vA = nA < fa.N, vB = nB < fa.N;
     f32x2 A[12];
-    decode2<SP>(R, pl.anc_in, A);
+    decode2<SP>(Ra, Rb, pl.anc_in, A);
     // the plane stride, re-derived each task on the scalar unit (hoisted, its plane offsets held SGPRs across the
     // loop and spilled)
     const int64_t ldl = (int64_t)sopaque((uint32_t)fa.ld);
     // the next task's state, in flight across this task's arithmetic; then the rows of the task after it
-    load_state_prefetch<SP>(prior, ldl, rA, true, R.a);
-    load_state_prefetch<SP>(prior, ldl, rB, true, R.b);
+    load_state_prefetch<SP>(prior, ldl, rA, true, Ra);
+    load_state_prefetch<SP>(prior, ldl, rB, true, Rb);
     rows_of(tk + 2 * nwaves, rA, rB);
     // ---- motion model (propagate, PE:543-588), both particles per instruction
     const Phx2 ph = philox_motion_pair((uint32_t)nA, (uint32_t)nB, (uint32_t)iter | (kTagMotion << 24), fa.flo, fa.fhi,

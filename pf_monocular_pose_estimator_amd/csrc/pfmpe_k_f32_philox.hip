@@ -11,6 +11,9 @@
 #ifndef PFMPE_WEIGH_MIN_WAVES
 #define PFMPE_WEIGH_MIN_WAVES 6  // k_propagate_weigh: >= 6 waves per SIMD (12/16-marker instances)
 #endif
+#ifndef PFMPE_WEIGH_PK_MIN_WAVES
+#define PFMPE_WEIGH_PK_MIN_WAVES 4  // k_weigh_pk<float>: 4 waves per SIMD (135 -> 128 VGPRs, no scratch)
+#endif
 #include "pfmpe_ctx.hpp"
 
 namespace pfmpe_impl {

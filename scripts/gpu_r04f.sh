@@ -4,6 +4,9 @@
 # packed pass (default) and without it (PFMPE_DIAG 4096).  Alternating, two rounds.  Logs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
 L=pf_monocular_pose_estimator_amd
+timeout -k 10 400 python -u -m pytest tests/test_gpu_weigh_pk.py tests/test_gpu_multi.py -k "pk or streaming" -x -q \
+  --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r04f_tests.log 2>&1 || { tail -20 gpurun_out/r04f_tests.log; exit 1; }
+tail -2 gpurun_out/r04f_tests.log
 run() {  # tag, bench args
   local tag=$1; shift
   timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 --cpu-frames 0 --worst-frames 0 --multi-sweep none \
