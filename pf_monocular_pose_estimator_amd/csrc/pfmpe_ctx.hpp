@@ -287,6 +287,7 @@ inline void klaunch(pfmpe_ctx* c, void (*kernel)(KArgs...), dim3 grid, dim3 bloc
 // host-synchronous entries (ROI, read-backs, initialisation, detector).  Every bracket is recorded on c->stream,
 // so waiting for the last one's end event completes them all.
 constexpr size_t kHarvestPairs = 256;
+constexpr size_t kEventPrealloc = 64;  // event pairs created when timing is switched on (PFMPE_OPT_TIMING)
 inline int harvest_timing(pfmpe_ctx* c) {
   if (c->ev_used == 0) return PFMPE_OK;
   HIPCHK(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].b));

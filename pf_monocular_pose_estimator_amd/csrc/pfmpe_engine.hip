@@ -358,6 +358,17 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       if (value < 0 || value > (1 << 20)) return fail(c, PFMPE_E_ARG, "set_option: timing period out of range");
       c->timing = (int)value;
       c->timing_frame = 0;
+      // the brackets' events are created now, not by the first timed frames: hipEventCreate inside a timed frame
+      // had added its cost to every bracket of a short run (the pool starts empty)
+      if (value > 0 && c->ev_pool.size() < kEventPrealloc) {
+        RET(set_device(c));
+        while (c->ev_pool.size() < kEventPrealloc) {
+          EventPair p{};
+          HIPCHK(c, hipEventCreate(&p.a));
+          HIPCHK(c, hipEventCreate(&p.b));
+          c->ev_pool.push_back(p);
+        }
+      }
       return PFMPE_OK;
     case 99:  // undocumented: diagnostic kernel switches for timing experiments
       c->diag = (int)value;
