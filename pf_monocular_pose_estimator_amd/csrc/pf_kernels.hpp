@@ -2491,22 +2491,32 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
   none.maxw = -INFINITY;
   none.minw = INFINITY;
   none.argmax = none.argmin = 0x7fffffff;
+  // wave 0 requests the control record together with the group partials (the record was written by an earlier
+  // launch; its load was a separate round trip after two barriers)
+  Ctrl c;
+  if (wv == 0) c = load_ctrl_wt(ctrl);
   for (int g = (int)threadIdx.x; g < ngrp; g += 64 * kTopWaves) gsm[g] = group_part(src, g, none, false);
   __syncthreads();
-  // tile totals of this iteration's group sums (used if this iteration turns out to be the kept one)
-  for (int t = wv; t < ntiles; t += kTopWaves) {
-    const int g = t * 64 + lane;
-    const double incl = wave_incl_sum(g < ngrp ? gsm[g].sum : 0.0);
-    if (lane == 63) tileT[t] = incl;
+  // tile totals of this iteration's group sums (used if this iteration turns out to be the kept one); each wave
+  // keeps its tiles' inclusive sums for the second pass
+  constexpr int kTilesPerWave = (kTopMaxTiles + kTopWaves - 1) / kTopWaves;
+  double inclT[kTilesPerWave];
+#pragma unroll
+  for (int i = 0; i < kTilesPerWave; ++i) {
+    const int t = wv + i * kTopWaves;
+    inclT[i] = 0.0;
+    if (t < ntiles) {  // wave-uniform
+      const int g = t * 64 + lane;
+      inclT[i] = wave_incl_sum(g < ngrp ? gsm[g].sum : 0.0);
+      if (lane == 63) tileT[t] = inclT[i];
+    }
   }
   __syncthreads();
-  Ctrl c;
   if (wv == 0) {  // propagate_top's head: this iteration's max / first argmax, best, exit rule
     double mv = -INFINITY;
     int mi = 0x7fffffff;
     for (int g = lane; g < ngrp; g += 64) cmb_max(mv, mi, gsm[g].maxw, gsm[g].argmax);
     wave_argmax(mv, mi);
-    c = load_ctrl_wt(ctrl);
     if (mv > c.best_max) {  // strict: PE:608
       c.best_max = mv;
       c.best_idx = mi;
@@ -2539,9 +2549,9 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
   if (!wide) return;
   const double S = S_sh;
   // per tile: G_g and the normalised group-start values' in-tile max scan (propagate_top's second pass)
-  double exl[(kTopMaxTiles + kTopWaves - 1) / kTopWaves];
+  double exl[kTilesPerWave];
 #pragma unroll
-  for (int i = 0; i < (kTopMaxTiles + kTopWaves - 1) / kTopWaves; ++i) {
+  for (int i = 0; i < kTilesPerWave; ++i) {
     const int t = wv + i * kTopWaves;
     exl[i] = -INFINITY;
     if (t < ntiles) {  // wave-uniform
@@ -2551,7 +2561,7 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
       q.zmax = -INFINITY;
       q.zmin = INFINITY;
       if (g < ngrp) q = gsm[g];
-      const double incl = wave_incl_sum(q.sum);
+      const double incl = inclT[i];  // the first pass's wave_incl_sum of the same values
       const double prev = wave_shr1(incl, 0.0);
       const double G = lane == 0 ? carryT[t] : carryT[t] + prev;
       double cm = -INFINITY;
@@ -2564,7 +2574,7 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < (kTopMaxTiles + kTopWaves - 1) / kTopWaves; ++i) {
+  for (int i = 0; i < kTilesPerWave; ++i) {
     const int t = wv + i * kTopWaves;
     if (t < ntiles) {
       double run = -INFINITY;
