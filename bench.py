@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--timing-period", type=int, default=0,
-                    help="HIP events bracket the kernels of every P-th timed frame (they serialise the stream); "
-                         "default max(1, steps // 10), so at least 10 launches are bracketed")
+                    help="HIP events bracket the kernels of every P-th timed frame; default ceil(steps / 4), so four "
+                         "frames are bracketed (a bracketed C2 frame costs ~12 us more: profiles/r04/c2_timing_*)")
     ap.add_argument("--occlude", type=int, default=0, choices=[0, 1],
                     help="time worst-case frames only: one LED hidden, so the reference's re-draw loop runs all "
                          "80 iterations (pose_estimator.cpp:535-616)")
@@ -319,8 +319,8 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
 def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args,
                         state_dtype=None, kernels=False):
     """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
-    every frame blocks on its record).  kernels: also bracket the kernels of every 10th timed frame with HIP
-    events and report their averages, the frame shape and the weighing pass."""
+    every frame blocks on its record).  kernels: also bracket the kernels of four timed frames with HIP
+    events (four of them, like the main line) and report their averages, the frame shape and the weighing pass."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
     st = syn.make_stream(cfg, warmup + steps)
     eng = pf.Engine(device=device, max_particles=cfg.N,
@@ -342,7 +342,7 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
             eng.step(f)
         if kernels:
             eng.reset_kernel_stats()
-            eng.set_option(pf.OPT_TIMING, max(1, steps // 10))
+            eng.set_option(pf.OPT_TIMING, max(1, -(-steps // 4)))
         t0 = time.perf_counter()
         outs = eng.step_batch(frames[warmup:])
         el = time.perf_counter() - t0
@@ -410,7 +410,7 @@ def main():
         eng.step(frames[i])
     eng.reset_kernel_stats()
     if not args.no_timing:
-        eng.set_option(pf.OPT_TIMING, args.timing_period or max(1, args.steps // 10))
+        eng.set_option(pf.OPT_TIMING, args.timing_period or max(1, -(-args.steps // 4)))
 
     if dist:
         dist.barrier()

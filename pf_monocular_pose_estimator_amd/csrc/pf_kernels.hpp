@@ -2787,8 +2787,20 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   const int first = __builtin_amdgcn_readfirstlane(ld.first_blk);
   const int nblk = __builtin_amdgcn_readfirstlane(ld.fa.nblk);
   const unsigned char* tab = ld.table;
+  // the map entries [first, first + nblk): 16-B stores of eight entries where a whole aligned group of eight is the
+  // stream's (a C4 stream's 39k entries were 153 two-byte stores per thread: 10 us of staging), single entries at
+  // the two ends.  boff is 16-B aligned (batch_layout).
   uint16_t* bm = (uint16_t*)(dev + boff);
-  for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
+  const int g0 = (first + 7) >> 3, g1 = (first + nblk) >> 3;  // whole groups of eight: [g0, g1)
+  if (g1 > g0) {
+    const uint32_t v = (uint32_t)s | ((uint32_t)s << 16);
+    uint4* bm16 = (uint4*)bm;
+    for (int g = g0 + (int)threadIdx.x; g < g1; g += kBlock) bm16[g] = make_uint4(v, v, v, v);
+    for (int b = first + (int)threadIdx.x; b < 8 * g0; b += kBlock) bm[b] = (uint16_t)s;
+    for (int b = 8 * g1 + (int)threadIdx.x; b < first + nblk; b += kBlock) bm[b] = (uint16_t)s;
+  } else {
+    for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
+  }
   const uintptr_t to = (uintptr_t)tab - (uintptr_t)dev;  // wraps above tbytes for bank tables
   if (to < tbytes) {
     const uint64_t* src = (const uint64_t*)(host + to);
