@@ -320,7 +320,7 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
                         state_dtype=None, kernels=False):
     """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
     every frame blocks on its record).  kernels: also bracket the kernels of four timed frames with HIP
-    events (four of them, like the main line) and report their averages, the frame shape and the weighing pass."""
+    events (as the main line does) and report their averages, the frame shape and the weighing pass."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
     st = syn.make_stream(cfg, warmup + steps)
     eng = pf.Engine(device=device, max_particles=cfg.N,
