@@ -51,8 +51,8 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
     ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
     ap.add_argument("--timing-period", type=int, default=0,
-                    help="HIP events bracket the kernels of every P-th timed frame; default ceil(steps / 4), so four "
-                         "frames are bracketed (a bracketed C2 frame costs ~12 us more: profiles/r04/c2_timing_*)")
+                    help="HIP events bracket the kernels of every P-th timed frame; default: two frames up to 40 "
+                         "timed frames, four beyond (a bracketed C2 frame costs ~12 us more, DESIGN.md §7)")
     ap.add_argument("--occlude", type=int, default=0, choices=[0, 1],
                     help="time worst-case frames only: one LED hidden, so the reference's re-draw loop runs all "
                          "80 iterations (pose_estimator.cpp:535-616)")
@@ -88,6 +88,14 @@ def parse():
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
     return ap.parse_args()
+
+
+def timing_period(steps: int) -> int:
+    """HIP-event sampling period: two bracketed frames up to 40 timed frames, four beyond.  A bracketed frame
+    (hipExtLaunchKernel with start / stop events) costs ~12 us more at C2, so the brackets are
+    kept few; their kernel averages agree with the rocprofv3 trace of the same command (profiles/r04/)."""
+    n = 2 if steps <= 40 else 4
+    return max(1, -(-steps // n))
 
 
 def algorithmic_bytes(S: int, N: int, k: float = 1.0) -> dict:
@@ -319,7 +327,7 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
 def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args,
                         state_dtype=None, kernels=False):
     """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
-    every frame blocks on its record).  kernels: also bracket the kernels of four timed frames with HIP
+    every frame blocks on its record).  kernels: also bracket the kernels of a few timed frames with HIP
     events (as the main line does) and report their averages, the frame shape and the weighing pass."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
     st = syn.make_stream(cfg, warmup + steps)
@@ -342,7 +350,7 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
             eng.step(f)
         if kernels:
             eng.reset_kernel_stats()
-            eng.set_option(pf.OPT_TIMING, max(1, -(-steps // 4)))
+            eng.set_option(pf.OPT_TIMING, timing_period(steps))
         prepared = eng.prepare_batch(frames[warmup:])
         t0 = time.perf_counter()
         outs = eng.run_batch(prepared)
@@ -411,7 +419,7 @@ def main():
         eng.step(frames[i])
     eng.reset_kernel_stats()
     if not args.no_timing:
-        eng.set_option(pf.OPT_TIMING, args.timing_period or max(1, -(-args.steps // 4)))
+        eng.set_option(pf.OPT_TIMING, args.timing_period or timing_period(args.steps))
 
     if dist:
         dist.barrier()
