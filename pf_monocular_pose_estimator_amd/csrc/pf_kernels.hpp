@@ -1472,7 +1472,8 @@ enum : int {
   kDiagNoPk = 4096,        // two-launch path: never the two-particles-per-lane pass k_weigh_pk (A/B, tests)
   kDiagCorruptDesc = 8192, // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
                            // staging check; the altered word is a key word, never a pointer)
-  kDiagNoDefer = 16384     // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
+  kDiagNoDefer = 16384,    // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
+  kDiagSplitTop = 32768    // more than one tile of groups: k_group + k_top_wide as two launches (A/B of k_group_top_wide)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -2617,6 +2618,34 @@ __global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T>
                                                           int iter) {
   extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries
   __shared__ TopWideLds tw;
+  top_wide_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, gsm, tw);
+}
+// k_group + k_top_wide as ONE launch (more than one tile of groups: C4's 611): block b's kTopWaves waves scan groups
+// kTopWaves * b + w exactly as k_group does (propagate_group: the group partials are stored write-through), every
+// wave drains its stores, the block makes ONE arrival on the top counter (ngrp / 16 arrivals instead of the ngrp
+// that made a per-group counter serialise, k_group's comment), and the last block runs top_wide_body, whose loads
+// of the group partials are write-through loads (group_part).  Saves a launch boundary; same functions, so the same
+// bits as the two launches.
+template <typename T, int RNG>
+__global__ __launch_bounds__(64 * kTopWaves) void k_group_top_wide(
+    const FrameArgsT<T> fa, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
+    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
+    uint32_t* __restrict__ tcount, int iter) {
+  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries (the last block's top)
+  __shared__ TopWideLds tw;
+  __shared__ int last;
+  if (ctrl->done) return;  // every block reads ctrl before it arrives, so before the top can rewrite it
+  const int slot = ctrl->cur_slot;
+  const int g = (int)blockIdx.x * kTopWaves + wave_id_u();
+  if (g < fa.ngrp)
+    (void)propagate_group<true>(fa.nblk, fa.gsz, g, slot ? part1 : part0, slot ? bscan1 : bscan0,
+                                slot ? gpart1 : gpart0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores landed before the arrival
+  __syncthreads();
+  if (threadIdx.x == 0) last = arrive_last(tcount, (int)gridDim.x) ? 1 : 0;
+  __syncthreads();
+  if (!last) return;
   top_wide_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, gsm, tw);
 }
 
