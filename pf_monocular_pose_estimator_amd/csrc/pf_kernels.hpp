@@ -1314,8 +1314,11 @@ __device__ __forceinline__ void bcast63(V& v, int& i) {
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
 // fl(k + U_k): the numerator of target r_k = fl(fl(k + U_k) / N)
-template <typename T, int RNG>
+// UNI: k is wave-uniform (a block-boundary evaluation); it is moved to an SGPR first, so the generator runs on the
+// scalar unit instead of issuing a whole wave's VALU stream for one lane
+template <typename T, int RNG, bool UNI = false>
 __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters, int64_t k) {
+  if (UNI) k = (int64_t)(int32_t)__builtin_amdgcn_readfirstlane((uint32_t)k);  // 0 <= k <= N < 2^31
   double U;
   if (RNG == kRngReference) {
     const uint64_t motion = fa.N > 2 ? (uint64_t)12 * (uint64_t)(fa.N - 2) * (uint64_t)iters : 0u;
@@ -1323,7 +1326,8 @@ __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters,
     const uint32_t g2 = lcg_next(g1);
     U = ref_uniform(ref_canonical(g1, g2), 0.0, 1.0);
   } else {
-    const U32x4 o = philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
+    const U32x4 o = UNI ? philox4x32_10_uniform((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1)
+                        : philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
     U = u53(o.x, o.y);
   }
   return (double)(int32_t)k + U;  // 0 <= k <= N < 2^31: one v_cvt_f64_i32 (exact)
@@ -1336,9 +1340,9 @@ __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters,
 // thr = fl(x*N)*2^-50 + 2^-1000 bounds N*ulp(x) from above with a wide margin (ulp(x) <= x*2^-52 for normal x;
 // the absolute term covers tiny x).  Between the two (a within ~2^-50 relative of x*N) the reference's own
 // division decides.  xn = fl(x*N), thr = fma(xn, 2^-50, 2^-1000): per call site, computed once.
-template <typename T, int RNG>
+template <typename T, int RNG, bool UNI = false>
 __device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, int64_t k, double x, double thr) {
-  const double a = target_num<T, RNG>(fa, iters, k);
+  const double a = target_num<T, RNG, UNI>(fa, iters, k);
   const double Nd = (double)fa.N;
   const double e = __builtin_fma(x, Nd, -a);
   if (e >= 0.0) return true;
@@ -1357,7 +1361,7 @@ __device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, in
 //   f > k 2^-51.
 // For N < 2^31 both bounds are below kEdge = 1e-6; inside that band (or for x N >= N) the neighbours
 // are scanned explicitly.
-template <typename T, int RNG>
+template <typename T, int RNG, bool UNI = false>
 __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int iters, double x) {
   constexpr double kEdge = 1e-6;
   const int64_t N = fa.N;
@@ -1370,20 +1374,20 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   if (!(fk < (double)N)) {  // x >= ~1: scan down from N
     int64_t k = N;
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
+    while (k > 0 && !target_le<T, RNG, UNI>(fa, iters, k - 1, x, thr)) --k;
     return k;
   }
   int64_t k = (int64_t)fk;
   const double f = xn - fk;
-  if (target_le<T, RNG>(fa, iters, k, x, thr)) {
+  if (target_le<T, RNG, UNI>(fa, iters, k, x, thr)) {
     ++k;
     if (1.0 - f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-      while (k < N && target_le<T, RNG>(fa, iters, k, x, thr)) ++k;
+      while (k < N && target_le<T, RNG, UNI>(fa, iters, k, x, thr)) ++k;
     }
   } else if (f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
+    while (k > 0 && !target_le<T, RNG, UNI>(fa, iters, k - 1, x, thr)) --k;
   }
   return k;
 }
@@ -1472,8 +1476,7 @@ enum : int {
   kDiagNoPk = 4096,        // two-launch path: never the two-particles-per-lane pass k_weigh_pk (A/B, tests)
   kDiagCorruptDesc = 8192, // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
                            // staging check; the altered word is a key word, never a pointer)
-  kDiagNoDefer = 16384,    // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
-  kDiagSplitTop = 32768    // more than one tile of groups: k_group + k_top_wide as two launches (A/B of k_group_top_wide)
+  kDiagNoDefer = 16384     // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -2620,34 +2623,6 @@ __global__ __launch_bounds__(64 * kTopWaves) void k_top_wide(const FrameArgsT<T>
   __shared__ TopWideLds tw;
   top_wide_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, gsm, tw);
 }
-// k_group + k_top_wide as ONE launch (more than one tile of groups: C4's 611): block b's kTopWaves waves scan groups
-// kTopWaves * b + w exactly as k_group does (propagate_group: the group partials are stored write-through), every
-// wave drains its stores, the block makes ONE arrival on the top counter (ngrp / 16 arrivals instead of the ngrp
-// that made a per-group counter serialise, k_group's comment), and the last block runs top_wide_body, whose loads
-// of the group partials are write-through loads (group_part).  Saves a launch boundary; same functions, so the same
-// bits as the two launches.
-template <typename T, int RNG>
-__global__ __launch_bounds__(64 * kTopWaves) void k_group_top_wide(
-    const FrameArgsT<T> fa, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
-    BlockScan* __restrict__ bscan0, BlockScan* __restrict__ bscan1, GroupPart* __restrict__ gpart0,
-    GroupPart* __restrict__ gpart1, GroupScan* __restrict__ gscan, Ctrl* __restrict__ ctrl,
-    uint32_t* __restrict__ tcount, int iter) {
-  extern __shared__ __attribute__((aligned(16))) GroupPart gsm[];  // ngrp entries (the last block's top)
-  __shared__ TopWideLds tw;
-  __shared__ int last;
-  if (ctrl->done) return;  // every block reads ctrl before it arrives, so before the top can rewrite it
-  const int slot = ctrl->cur_slot;
-  const int g = (int)blockIdx.x * kTopWaves + wave_id_u();
-  if (g < fa.ngrp)
-    (void)propagate_group<true>(fa.nblk, fa.gsz, g, slot ? part1 : part0, slot ? bscan1 : bscan0,
-                                slot ? gpart1 : gpart0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's write-through stores landed before the arrival
-  __syncthreads();
-  if (threadIdx.x == 0) last = arrive_last(tcount, (int)gridDim.x) ? 1 : 0;
-  __syncthreads();
-  if (!last) return;
-  top_wide_body<T, RNG>(fa, gpart0, gpart1, gscan, ctrl, iter, gsm, tw);
-}
 
 // ---- launch 1 of the two-launch path: motion + projection + likelihood, one particle per thread.
 // One block's work (block `blk` of its stream), shared by the one-stream kernel and the batched kernel
@@ -3150,7 +3125,16 @@ __device__ __forceinline__ void resample_phase(
   if (lane == 63) sh.hi[wv] = hi;
   __syncthreads();
   int lo = wave_shr1(hi, 0);
-  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : sh.hi[wv - 1];
+  if (wv == 0) {  // the block's first count needs F(rin): block-uniform, so evaluated on the scalar unit (issued as
+                  // a lane-0 VALU stream it cost wave 0 about 150 instructions, ~11 % of the kernel's VALU)
+    const uint64_t rb = (uint64_t)__double_as_longlong(rin);
+    const double ru = __longlong_as_double((long long)((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)rb) |
+                                                       ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(rb >> 32)) << 32)));
+    const int lo0 = (int)count_targets<T, RNG, true>(fa, __builtin_amdgcn_readfirstlane(iters), ru);
+    if (lane == 0) lo = lo0;
+  } else if (lane == 0) {
+    lo = sh.hi[wv - 1];
+  }
   const int cntn = valid ? hi - lo : 0;
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 11, rt_now());
   if (counts && valid) counts[n] = (uint32_t)cntn;

@@ -484,13 +484,6 @@ struct Seq {
           klaunch(c, k_group_top<T, RNG>, dim3(fa.ngrp), dim3(64), 0, fa, c->d_part[0], c->d_part[1], c->d_bscan[0],
                   c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, tcount, iter);
         });
-      const bool wide = staged && fa.ngrp <= 64 * kTopMaxTiles && !(c->diag & kDiagSerialTop);
-      if (wide && !(c->diag & kDiagSplitTop))  // the group scans and the wide top in one launch (last arriver)
-        return launch_ext(c, PFMPE_K_AUX, [&] {
-          klaunch(c, k_group_top_wide<T, RNG>, dim3((fa.ngrp + kTopWaves - 1) / kTopWaves), dim3(64 * kTopWaves), glds,
-                  fa, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1],
-                  c->d_gscan, c->d_ctrl, tcount, iter);
-        });
       return launch_ext(c, PFMPE_K_AUX, [&] {
         klaunch(c, k_group<T>, dim3(fa.ngrp), dim3(64), 0, fa, c->d_part[0], c->d_part[1],
                            c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], (const Ctrl*)c->d_ctrl);
