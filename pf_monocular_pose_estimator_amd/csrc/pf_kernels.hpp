@@ -145,7 +145,7 @@ struct LdsConst {
 struct Ctrl {
   double best_max;   // highestProb
   double S;          // probPartSum of the kept iteration
-  double Rmax;       // max normalised cumulative weight (running max at the last particle)
+  double invS;       // fl(1 / S): k_resample's divisions by S as a product and two fma corrections (div_by_S)
   int32_t done, has_best, best_idx, best_iter, best_slot, cur_slot;
   int32_t iters, kept_slot, kept_iter, accepted, most_likely_idx, pad0;
   int64_t K_total;   // number of stratified targets that find a particle
@@ -1252,6 +1252,31 @@ __device__ __forceinline__ void wave_argmax<int>(int& v, int& i) {
 // Deterministic block inclusive scan: pre_w = ((0 + t_0) + t_1) + ... over earlier waves' totals, then
 // incl = pre_w + (wave inclusive).  k_propagate_weigh derives its partial extrema with exactly this
 // association, so both launches see bit-identical prefixes.  sh: >= kWaves doubles.
+// The wave scan of fp32 weights on the 2^-21 grid as integers.  Every weight of an M >= 4 frame is a multiple of
+// 2^-21 (each score term Mt + q^2 is >= 4, so every partial score, the integer penalties subtracted, is too), so
+// with 0 <= w < 32 in the wave, w * 2^21 is an integer below 2^26 and every 64-lane prefix lies below 2^32: the u32
+// scan is the exact prefix sum, which wave_incl_sum's fp64 partial sums (at most 32 significant bits) also are.
+// One v_add_u32_dpp per step instead of two v_mov_b32_dpp and a v_add_f64.
+__device__ __forceinline__ double wave_incl_sum_fx(float w) {
+  uint32_t x = (uint32_t)(w * 0x1p21f);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kDppRowShr1, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kDppRowShr2, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kDppRowShr4, 0xf, 0xf, true);
+  x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, kDppRowShr8, 0xf, 0xf, true);
+  x += dpp_u32<kDppBcast15, 0xa>(x, 0u);
+  x += dpp_u32<kDppBcast31, 0xc>(x, 0u);
+  return (double)x * 0x1p-21;
+}
+// block inclusive prefix from the wave's inclusive scan wi (the earlier waves' totals through LDS)
+__device__ __forceinline__ void block_incl_from_wave(double wi, double& incl, double* sh) {
+  if (lane_id() == 63) sh[wave_id()] = wi;
+  __syncthreads();
+  double pre = 0.0;
+  const int wv = wave_id_u();
+#pragma clang loop unroll(disable)
+  for (int w = 0; w < wv; ++w) pre = pre + sh[w];  // a scalar trip count: no per-wave select chain
+  incl = pre + wi;
+}
 __device__ __forceinline__ void block_incl_sum(double v, double& incl, double* sh) {
   const double wi = wave_incl_sum(v);
   if (lane_id() == 63) sh[wave_id()] = wi;
@@ -1311,6 +1336,20 @@ __device__ __forceinline__ void bcast63(V& v, int& i) {
   i = lane_value(i, 63);
 }
 
+// fl(a / b) without the fp64 division: y = fl(1 / b) (Ctrl::invS, one division per frame), q0 = fl(a y), then two
+// Newton corrections with fma residuals.  After the first, q1 is a faithful approximation of a / b, so its residual
+// a - b q1 is exact, and fl(q1 + r1 y) = fl(a / b) (Markstein's theorem: y correctly rounded, no overflow or
+// underflow; tests/test_div_by_s.py checks 10^7 cases against IEEE division).  Callers use it only where the
+// quotient is in [0, ~1] and b is a normal positive double (fp32 weights, no negative weight in the wave), and
+// keep the IEEE division otherwise.
+__device__ __forceinline__ double div_by_S(double a, double b, double y) {
+  const double q0 = a * y;
+  const double r0 = __builtin_fma(-b, q0, a);
+  const double q1 = __builtin_fma(r0, y, q0);
+  const double r1 = __builtin_fma(-b, q1, a);
+  return __builtin_fma(r1, y, q1);
+}
+
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
 // fl(k + U_k): the numerator of target r_k = fl(fl(k + U_k) / N)
@@ -1345,9 +1384,15 @@ __device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, in
   const double a = target_num<T, RNG, UNI>(fa, iters, k);
   const double Nd = (double)fa.N;
   const double e = __builtin_fma(x, Nd, -a);
-  if (e >= 0.0) return true;
-  if (-e > thr) return false;
-  return a / Nd <= x;  // the reference's rounding (PE:674-679 compares the divided target)
+  bool le = e >= 0.0;
+  // the band: the reference's rounding decides (PE:674-679 compares the divided target).  Behind a wave-uniform
+  // test: as a plain `return a / Nd <= x` the compiler evaluated the fp64 division for every lane with e < 0
+  // (about half of them), i.e. in every wave of k_resample
+  const bool band = !le && !(-e > thr);
+  if (__builtin_amdgcn_ballot_w64(band)) {
+    if (band) le = a / Nd <= x;
+  }
+  return le;
 }
 
 // F(x) = #{k : r_k <= x}.  r_k is non-decreasing in k, so target k finds the first particle i whose
@@ -1377,7 +1422,7 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
     while (k > 0 && !target_le<T, RNG, UNI>(fa, iters, k - 1, x, thr)) --k;
     return k;
   }
-  int64_t k = (int64_t)fk;
+  int64_t k = (int64_t)(int32_t)fk;  // 0 <= fk < N < 2^31: one v_cvt_i32_f64 (an int64 conversion is five)
   const double f = xn - fk;
   if (target_le<T, RNG, UNI>(fa, iters, k, x, thr)) {
     ++k;
@@ -1801,7 +1846,7 @@ __device__ __forceinline__ Ctrl zero_ctrl() {
   Ctrl z;
   z.best_max = 0.0;
   z.S = 0.0;
-  z.Rmax = 0.0;
+  z.invS = 0.0;
   z.done = z.has_best = z.best_idx = z.best_iter = z.best_slot = z.cur_slot = 0;
   z.iters = z.kept_slot = z.kept_iter = z.accepted = z.most_likely_idx = z.pad0 = 0;
   z.K_total = 0;
@@ -2043,7 +2088,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
     wave_argmin(anv, ani);
     const double highest = c.has_best ? c.best_max : 0.0;
     c.S = S;
-    c.Rmax = run;
+    c.invS = 1.0 / S;
     c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
     if (c.accepted) {
       c.most_likely_idx = c.best_idx;
@@ -2130,19 +2175,20 @@ __device__ __forceinline__ double wave_total_lane63(double x) {
   return x;
 }
 // max of a float over the wave as order-preserving integers (v_max_i32: no NaN canonicalisation per step; the
-// weights are never NaN); the result is the maximum's exact bits.  Rows are combined through lane reads.
+// weights are never NaN); the result is the maximum's exact bits.  Rows are combined by the two row broadcasts.
 __device__ __forceinline__ int f32_sortable(float f) {
   const int b = (int)__float_as_uint(f);
   return b ^ ((b >> 31) & 0x7fffffff);
 }
 __device__ __forceinline__ float wave_max_f32(float x) {
   int k = f32_sortable(x);
-  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, false));
-  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, false));
-  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, false));
-  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, false));
-  k = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
-          max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, true));  // (folds into v_max_i32_dpp)
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, true));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, true));
+  k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, true));
+  k = max(k, dpp<kDppBcast15, 0xa>(k, INT_MIN));
+  k = max(k, dpp<kDppBcast31, 0xc>(k, INT_MIN));
+  k = __builtin_amdgcn_readlane(k, 63);
   return __uint_as_float((uint32_t)(k ^ ((k >> 31) & 0x7fffffff)));  // the map is an involution
 }
 
@@ -2464,7 +2510,7 @@ __global__ __launch_bounds__(64) void k_top(const FrameArgsT<T> fa, GroupPart* _
 // carried parts stay serial, in wave 0 and in the same order: S = ((0 + T_0) + T_1) + ... over the tile
 // totals T_t (each the last lane of the tile's wave_incl_sum, as in propagate_top), the carry into tile t,
 // and the running max over earlier tiles (a fold of `tm > run ? tm : run`, which ignores NaN and is the max
-// of the rest: order-free).  So G_g, Gin_g, S, Rmax and the record are bit-identical to propagate_top's.
+// of the rest: order-free).  So G_g, Gin_g, S, invS and the record are bit-identical to propagate_top's.
 // Non-final iterations, and a final iteration whose kept partials are an earlier iteration's (not staged),
 // run propagate_top itself in wave 0.
 constexpr int kTopWaves = 16;
@@ -2589,7 +2635,7 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
     }
   }
   if (wv != 0) return;
-  // propagate_top's tail: Rmax, the kept iteration's argmax / argmin, accept, the record
+  // propagate_top's tail: invS, the kept iteration's argmax / argmin, accept, the record
   double run = -INFINITY;
   for (int u = 0; u < ntiles; ++u) run = tileM[u] > run ? tileM[u] : run;
   if (S == 0.0) run = -INFINITY;
@@ -2603,7 +2649,7 @@ __device__ __forceinline__ void top_wide_body(const FrameArgsT<T>& fa, GroupPart
   wave_argmin(anv, ani);
   const double highest = c.has_best ? c.best_max : 0.0;
   c.S = S;
-  c.Rmax = run;
+  c.invS = 1.0 / S;
   c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
   if (c.accepted) {
     c.most_likely_idx = c.best_idx;
@@ -3089,17 +3135,35 @@ __device__ __forceinline__ void resample_phase(
   const double S = c.S;
   const int64_t Kt = c.K_total;
 
+  // fp32 weights of an M >= 4 frame, all in [0, 32) in this wave: the in-wave prefix as a fixed-point integer scan
+  // (wave_incl_sum_fx, exact and equal to the fp64 scan); otherwise the fp64 scan.  Wave-uniform choice.
+  const bool fx = std::is_same<T, float>::value && fa.M >= 4 && __ballot(valid && !(wd >= 0.0 && wd < 32.0)) == 0;
+  double wi;
+  if (fx)
+    wi = wave_incl_sum_fx((float)wd);
+  else
+    wi = wave_incl_sum(wd);
   double incl;
-  block_incl_sum(wd, incl, sh.sum);
+  block_incl_from_wave(wi, incl, sh.sum);
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 10, rt_now());
-  const double cn = (gs.G + (bs.E + incl)) / S;
+  // fp32 weights, none negative in the wave, S a normal positive double: every quotient below lies in [0, ~1], so
+  // div_by_S is exact (wave-uniform choice; the IEEE division otherwise)
+  const bool nonneg = fx || __ballot(valid && wd < 0.0) == 0;
+  const bool recip = std::is_same<T, float>::value && nonneg && S > 0x1p-1000 && S < 0x1p1000;
+  const double num = gs.G + (bs.E + incl);
+  double cn;
+  if (recip)
+    cn = div_by_S(num, S, c.invS);
+  else
+    cn = num / S;
   // running max of c seeded by the exact running max at the block start:
   // max(Gin_g, fl(fl(G_g + zin_b)/S)); zin_b = -inf (S > 0) / +inf (S < 0) for a group's first block
   const double zin = S > 0.0 ? bs.zin_max : bs.zin_min;
   const bool first_in_group = (blk % fa.gsz) == 0;
   double rin = gs.Gin;
   if (!first_in_group) {
-    const double cz = (gs.G + zin) / S;
+    const double zn = gs.G + zin;
+    const double cz = recip && zn >= 0.0 && zn <= 2.0 * S ? div_by_S(zn, S, c.invS) : zn / S;
     rin = cz > rin ? cz : rin;
   }
   // Running max of c over the wave.  With S > 0 and no negative weight in the wave, c is non-decreasing over
@@ -3108,7 +3172,7 @@ __device__ __forceinline__ void resample_phase(
   // Otherwise the fp64 max scan (wave-uniform branch).
   const uint64_t vmask = __ballot(valid);
   double rm;
-  if (S > 0.0 && __ballot(valid && wd < 0.0) == 0) {
+  if (S > 0.0 && nonneg) {
     const double last = vmask ? lane_value(cn, 63 - __builtin_clzll(vmask)) : -INFINITY;
     rm = valid ? cn : last;
   } else {
@@ -3164,13 +3228,16 @@ __device__ __forceinline__ void resample_phase(
                           // (count, index) as ONE int key, count * 256 + (255 - thread), whose max
                           // is the max count at its lowest index; integer max needs no canonicalising, and the
                           // rows are combined through four lane reads
+      // (bound_ctrl: every lane of these patterns has a source, so each move folds into a v_max_i32_dpp; the row
+      // results are carried to lane 63 by the two row broadcasts and read once)
       int k = valid ? cntn * 256 + (255 - (int)threadIdx.x) : -1;
-      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, false));
-      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, false));
-      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, false));
-      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, false));
-      k = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
-              max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, true));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, true));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, true));
+      k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, true));
+      k = max(k, dpp<kDppBcast15, 0xa>(k, INT_MIN));
+      k = max(k, dpp<kDppBcast31, 0xc>(k, INT_MIN));
+      k = __builtin_amdgcn_readlane(k, 63);
       cv = k < 0 ? -1 : k >> 8;
       ci = k < 0 ? 0x7fffffff : blk * kBlock + 255 - (k & 255);
     } else {
@@ -3918,7 +3985,7 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
     if (S == 0.0) run = -INFINITY;
     const double highest = c.has_best ? c.best_max : 0.0;
     c.S = S;
-    c.Rmax = run;
+    c.invS = 1.0 / S;
     c.accepted = (S != 0.0 && highest > fa.accept_thr) ? 1 : 0;  // PE:633
     if (c.accepted) {
       c.most_likely_idx = c.best_idx;

@@ -227,16 +227,33 @@ __device__ __forceinline__ void pk_wave_partial(float w, bool valid, int nbase, 
   const uint64_t negm = __builtin_amdgcn_ballot_w64(valid && w < 0.0f);
   if (vmask == ~0ull && negm == 0) {
     const double x = (double)w;
-    const double wi = wave_total_lane63(x);
     int k = __float_as_int(w);
-    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, false));
-    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, false));
-    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, false));
-    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, false));
-    const int mxb = max(max(__builtin_amdgcn_readlane(k, 0), __builtin_amdgcn_readlane(k, 16)),
-                        max(__builtin_amdgcn_readlane(k, 32), __builtin_amdgcn_readlane(k, 48)));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, true));
+    // (bound_ctrl: every lane of these patterns has a source, and with it the moves fold into v_max_i32_dpp)
+    k = max(k, dpp<kDppBcast15, 0xa>(k, INT_MIN));  // row totals carried into rows 1 / 3, then 2 / 3: lane 63
+    k = max(k, dpp<kDppBcast31, 0xc>(k, INT_MIN));
+    const int mxb = __builtin_amdgcn_readlane(k, 63);
     const uint64_t bx = __builtin_amdgcn_ballot_w64(__float_as_int(w) == mxb);
     const int ix = nbase + (int)__builtin_ctzll(bx);
+    // the total: with every weight below 32 (the usual case: at most 5 * 6), as integers on the 2^-21 grid every
+    // weight of this pass lies on (wave_incl_sum_fx, pf_kernels.hpp): the exact sum, which is what the fp64
+    // butterfly yields too (its partial sums need at most 32 significant bits)
+    double wi;
+    if (mxb < 0x42000000) {  // 32.0f; a scalar branch
+      uint32_t t = (uint32_t)(w * 0x1p21f);
+      t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, kDppQuadXor1, 0xf, 0xf, true);
+      t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, kDppQuadXor2, 0xf, 0xf, true);
+      t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, kDppRowHalfMirror, 0xf, 0xf, true);
+      t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, kDppRowMirror, 0xf, 0xf, true);
+      t += dpp_u32<kDppBcast15, 0xa>(t, 0u);
+      t += dpp_u32<kDppBcast31, 0xc>(t, 0u);
+      wi = (double)(uint32_t)__builtin_amdgcn_readlane((int)t, 63) * 0x1p-21;
+    } else {
+      wi = wave_total_lane63(x);
+    }
     if (lane == 63) {
       dst->sum = wi;
       dst->maxrel = wi;

@@ -22,6 +22,7 @@ constexpr int kRounds = 256;
     uint32_t o32;                                                                                  \
     float of;                                                                                      \
     double od;                                                                                     \
+    const uint64_t m64 = __builtin_amdgcn_ballot_w64((threadIdx.x & 3) != 0);                     \
     __syncthreads();                                                                               \
     const uint64_t t0 = __builtin_amdgcn_s_memtime();                                              \
     for (int r = 0; r < kRounds; ++r) {                                                            \
@@ -30,7 +31,7 @@ constexpr int kRounds = 256;
     const uint64_t t1 = __builtin_amdgcn_s_memtime();                                              \
     if ((threadIdx.x & 63) == 0) cyc[blockIdx.x * 4 + (threadIdx.x >> 6)] = t1 - t0;               \
     (void)o64; (void)o32; (void)of; (void)od; (void)fa; (void)fb; (void)fc; (void)da; (void)db;    \
-    (void)a; (void)b; (void)c;                                                                     \
+    (void)a; (void)b; (void)c; (void)m64;                                                          \
   }
 
 DEFK(k_mad_u64, asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, 0" : "=v"(o64) : "v"(a), "v"(b) : "s0", "s1");)
@@ -59,6 +60,36 @@ DEFK(k_cndmask, asm volatile("v_cndmask_b32 %0, %1, %2, vcc" : "=v"(o32) : "v"(a
 DEFK(k_cmp_u32, asm volatile("v_cmp_eq_u32 vcc, %0, %1" :: "v"(a), "v"(b) : "vcc");)
 DEFK(k_cmp_e64, asm volatile("v_cmp_eq_u32 %0, %1, %2" : "=s"(o64) : "v"(a), "v"(b));)
 
+DEFK(k_add_f32, asm volatile("v_add_f32 %0, %1, %2" : "=v"(of) : "v"(fa), "v"(fb));)
+DEFK(k_mul_f32, asm volatile("v_mul_f32 %0, %1, %2" : "=v"(of) : "v"(fa), "v"(fb));)
+DEFK(k_fma_f32_s, asm volatile("v_fma_f32 %0, %1, %2, %3" : "=v"(of) : "v"(fa), "s"(fc), "v"(fb));)
+DEFK(k_mov_b32, asm volatile("v_mov_b32 %0, %1" : "=v"(o32) : "v"(a));)
+DEFK(k_cnd_e64, asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(o32) : "v"(a), "v"(b), "s"(m64));)
+DEFK(k_cmp_cnd, asm volatile("v_cmp_gt_u32 vcc, %1, %2\n\tv_cndmask_b32 %0, %1, %2, vcc" : "=v"(o32) : "v"(a), "v"(b) : "vcc");)
+DEFK(k_cmp_cnd_s, asm volatile("v_cmp_gt_u32 %0, %2, %3\n\tv_cndmask_b32_e64 %1, %2, %3, %0" : "=&s"(o64), "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_add_u32, asm volatile("v_add_u32 %0, %1, %2" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_and_b32, asm volatile("v_and_b32 %0, %1, %2" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_xor_b32, asm volatile("v_xor_b32 %0, %1, %2" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_or3_b32, asm volatile("v_or3_b32 %0, %1, %2, %3" : "=v"(o32) : "v"(a), "v"(b), "v"(c));)
+DEFK(k_lshl_add, asm volatile("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_alignbit, asm volatile("v_alignbit_b32 %0, %1, %2, 11" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_max_i32, asm volatile("v_max_i32 %0, %1, %2" : "=v"(o32) : "v"(a), "v"(b));)
+DEFK(k_add3_u32, asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(o32) : "v"(a), "v"(b), "v"(c));)
+DEFK(k_mad_u24, asm volatile("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o32) : "v"(a), "v"(b), "v"(c));)
+DEFK(k_cvt_f32_u32, asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(of) : "v"(a));)
+DEFK(k_cvt_f32_f16, asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(of) : "v"(a));)
+DEFK(k_mul_f64, asm volatile("v_mul_f64 %0, %1, %2" : "=v"(od) : "v"(da), "v"(db));)
+DEFK(k_floor_f64, asm volatile("v_floor_f64 %0, %1" : "=v"(od) : "v"(da));)
+DEFK(k_exp_f32, asm volatile("v_exp_f32 %0, %1" : "=v"(of) : "v"(fa));)
+DEFK(k_cmp_f32_s, asm volatile("v_cmp_gt_f32 %0, %1, %2" : "=s"(o64) : "v"(fa), "v"(fb));)
+DEFK(k_rfl, asm volatile("v_readfirstlane_b32 %0, %1" : "=s"(o32) : "v"(a));)
+DEFK(k_perm, asm volatile("v_perm_b32 %0, %1, %2, %3" : "=v"(o32) : "v"(a), "v"(b), "v"(c));)
+DEFK(k_bfe, asm volatile("v_bfe_u32 %0, %1, 3, 10" : "=v"(o32) : "v"(a));)
+DEFK(k_pk_fma_sel, asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(o64) : "v"(da), "v"(db), "v"(da));)
+DEFK(k_fma_pair, asm volatile("v_fma_f32 %0, %1, %2, %3\n\tv_fma_f32 %0, %2, %3, %1" : "=&v"(of) : "v"(fa), "v"(fb), "v"(fc));)
+DEFK(k_mad_mix2, asm volatile("v_mad_u64_u32 %0, s[0:1], %2, %3, 0\n\tv_fma_f32 %1, %4, %5, %4" : "=&v"(o64), "=&v"(of) : "v"(a), "v"(b), "v"(fa), "v"(fb) : "s0", "s1");)
+DEFK(k_dpp_add, asm volatile("v_add_f32_dpp %0, %1, %2 row_shr:1 row_mask:0xf bank_mask:0xf" : "=v"(of) : "v"(fa), "v"(fb));)
+
 typedef void (*Kfn)(uint64_t*, uint32_t);
 struct Entry {
   const char* name;
@@ -76,6 +107,16 @@ int main() {
       {"v_mov_b32_dpp", k_mov_dpp},   {"v_max_i32_dpp", k_max_dpp},   {"v_readlane_b32", k_readlane},
       {"v_cvt_pk_f16_f32", k_cvt_pk_f16}, {"v_cndmask_b32", k_cndmask}, {"v_cmp_eq_u32 (vcc)", k_cmp_u32},
       {"v_cmp_eq_u32 (sgpr)", k_cmp_e64},
+      {"v_add_f32", k_add_f32}, {"v_mul_f32", k_mul_f32}, {"v_fma_f32 (sgpr src)", k_fma_f32_s},
+      {"v_mov_b32", k_mov_b32}, {"v_cndmask_b32_e64 (s mask)", k_cnd_e64}, {"cmp+cndmask vcc (2 ins)", k_cmp_cnd},
+      {"cmp+cndmask sgpr (2 ins)", k_cmp_cnd_s}, {"v_add_u32", k_add_u32}, {"v_and_b32", k_and_b32},
+      {"v_xor_b32", k_xor_b32}, {"v_or3_b32", k_or3_b32}, {"v_lshl_add_u32", k_lshl_add},
+      {"v_alignbit_b32", k_alignbit}, {"v_max_i32", k_max_i32}, {"v_add3_u32", k_add3_u32},
+      {"v_mad_u32_u24", k_mad_u24}, {"v_cvt_f32_u32", k_cvt_f32_u32}, {"v_cvt_f32_f16", k_cvt_f32_f16},
+      {"v_mul_f64", k_mul_f64}, {"v_floor_f64", k_floor_f64}, {"v_exp_f32", k_exp_f32},
+      {"v_cmp_gt_f32 (sgpr)", k_cmp_f32_s}, {"v_readfirstlane_b32", k_rfl}, {"v_perm_b32", k_perm},
+      {"v_bfe_u32", k_bfe}, {"v_pk_fma_f32 op_sel_hi", k_pk_fma_sel}, {"2x v_fma_f32 dep (2 ins)", k_fma_pair},
+      {"mad_u64 + fma_f32 (2 ins)", k_mad_mix2}, {"v_add_f32_dpp", k_dpp_add},
   };
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return 1;
