@@ -212,20 +212,20 @@ __device__ __forceinline__ void grid_walk(const unsigned char* ents, uint32_t re
 
 // One 64-particle wave partial (BlockPart: wave_weight_partials' values, k_weigh_stream's record) of fp32 weights
 // w of particles nbase + lane.  The steady state (every lane valid, no negative weight) is computed directly:
-//  * the total by wave_total_lane63 (the scan's lane-63 value, bit for bit); it is also the maximum in-wave
-//    prefix (non-negative addends: the prefix is lane-monotone), and lane 0's weight the minimum;
+//  * the total: the scan's lane-63 value, bit for bit (as integers on the 2^-21 grid when every weight is below
+//    32, else wave_total_lane63); it is also the maximum in-wave prefix (non-negative addends: the prefix is
+//    lane-monotone), and lane 0's weight the minimum;
 //  * the maximum weight as the integer maximum of the weights' bits (no weight is NaN or -0: the score adds
 //    positive terms to +0 and subtracts penalties, and fl(x - x) = +0, so the bits of non-negative weights
-//    order like their values), DPP max steps across quads and rows, then the four row results;
+//    order like their values), DPP max steps across quads and rows, then the two row broadcasts to lane 63;
 //  * the first lane holding it by ballot: argmax = nbase + that lane;
 //  * lane 63 stores {sum, maxrel} from its own registers, lane 0 {minrel, maxw, minw = +inf, argmax,
 //    argmin = none}.
 // Anything else (a partial wave past N, a negative weight) takes wave_weight_partials as k_weigh_stream does.
-__device__ __forceinline__ void pk_wave_partial(float w, bool valid, int nbase, BlockPart* __restrict__ dst) {
+// full: every particle of the task is below N (wave-uniform, decided on the scalar unit: no validity ballots).
+__device__ __forceinline__ void pk_wave_partial(float w, bool valid, bool full, int nbase, BlockPart* __restrict__ dst) {
   const int lane = lane_id();
-  const uint64_t vmask = __builtin_amdgcn_ballot_w64(valid);
-  const uint64_t negm = __builtin_amdgcn_ballot_w64(valid && w < 0.0f);
-  if (vmask == ~0ull && negm == 0) {
+  if (full && __builtin_amdgcn_ballot_w64(w < 0.0f) == 0) {
     const double x = (double)w;
     int k = __float_as_int(w);
     k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, true));
@@ -542,13 +542,20 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
     // Eigen's visitor starts at coeff(0, 0): a NaN distance there gives weight 0 (blob 0 finite: host check)
     if (__builtin_isunordered(u[0].x, v[0].x)) wA = 0.0f;
     if (__builtin_isunordered(u[0].y, v[0].y)) wB = 0.0f;
-    if (!vA) wA = 0.0f;
-    if (!vB) wB = 0.0f;
-    if (vA) wout[nA] = wA;
-    if (vB) wout[nB] = wB;
-    // ---- the two wave partials (k_weigh_stream's, one per 64 particles)
-    pk_wave_partial(wA, vA, tk * 128, parts + (size_t)tk * 2);
-    pk_wave_partial(wB, vB, tk * 128 + 64, parts + (size_t)tk * 2 + 1);
+    // ---- the weights and the two wave partials (k_weigh_stream's, one per 64 particles).  full (scalar): every
+    // particle of the task is below N, so no per-lane validity selects, predicated stores or validity ballots
+    const bool full = (tk + 1) * 128 <= fa.N;
+    if (full) {
+      wout[nA] = wA;
+      wout[nB] = wB;
+    } else {
+      if (!vA) wA = 0.0f;
+      if (!vB) wB = 0.0f;
+      if (vA) wout[nA] = wA;
+      if (vB) wout[nB] = wB;
+    }
+    pk_wave_partial(wA, vA, full, tk * 128, parts + (size_t)tk * 2);
+    pk_wave_partial(wB, vB, full, tk * 128 + 64, parts + (size_t)tk * 2 + 1);
   }
 }
 
