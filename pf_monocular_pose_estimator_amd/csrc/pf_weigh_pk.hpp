@@ -366,6 +366,12 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
   for (; tk < ntask; tk += nwaves) {
     const int nA = tk * 128 + lane, nB = nA + 64;
     const bool vA = nA < fa.N, vB = nB < fa.N;
+    // ---- motion model (propagate, PE:543-588), both particles per instruction.  The draws come first: they need
+    // no memory, so the wait for this task's prefetched state (and, the loop's waits being conservative, for the
+    // previous task's stores) sits after ~130 instructions of the generator instead of at the top of the loop
+    const Phx2 ph = philox_motion_pair((uint32_t)nA, (uint32_t)nB, (uint32_t)iter | (kTagMotion << 24), fa.flo, fa.fhi,
+                                       fa.key0, fa.key1);
+    __builtin_amdgcn_sched_barrier(0);  // the scheduler would otherwise pull the decode (and its wait) back up
     f32x2 A[12];
     decode2<SP>(Ra, Rb, pl.anc_in, A);
     // the plane stride, re-derived each task on the scalar unit (hoisted, its plane offsets held SGPRs across the
@@ -375,9 +381,6 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
     load_state_prefetch<SP>(prior, ldl, rA, true, Ra);
     load_state_prefetch<SP>(prior, ldl, rB, true, Rb);
     rows_of(tk + 2 * nwaves, rA, rB);
-    // ---- motion model (propagate, PE:543-588), both particles per instruction
-    const Phx2 ph = philox_motion_pair((uint32_t)nA, (uint32_t)nB, (uint32_t)iter | (kTagMotion << 24), fa.flo, fa.fhi,
-                                       fa.key0, fa.key1);
     f32x2 d[6];
     {
       float fa6[6], fb6[6];
