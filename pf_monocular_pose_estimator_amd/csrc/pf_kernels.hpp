@@ -176,6 +176,12 @@ struct alignas(16) GroupScan {
 struct alignas(8) CountPart {
   int32_t maxcount, idx;
 };
+// winner keys of the one-stream two-launch frame (k_resample -> k_resample_final): unsigned max of
+// count << 32 | (2^31 - 1 - index) is the max count at its lowest index; 0 (count 0 at no index) is the identity
+constexpr int kWinShards = 64;
+__host__ __device__ __forceinline__ unsigned long long win_key(int count, int idx) {
+  return ((unsigned long long)(uint32_t)count << 32) | (uint32_t)(0x7fffffff - idx);
+}
 
 // frame record written by the final wave into pinned host memory: the pfmpe_frame_out layout, then the
 // kept slot and the publication tag (2 * frame sequence + finished)
@@ -3121,7 +3127,8 @@ __device__ __forceinline__ void resample_phase(
     const LdsBlobs<T>& tb, Cand* __restrict__ cand, double* __restrict__ mlpose,
     CountPart* __restrict__ cpart, CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount,
     uint32_t* __restrict__ tcount, uint32_t* __restrict__ counts, RecOut* __restrict__ out, int32_t seq,
-    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk, const RawState<SP>* raw_in = nullptr) {
+    uint64_t* __restrict__ stamps, uint32_t* __restrict__ flat, int blk, const RawState<SP>* raw_in = nullptr,
+    unsigned long long* __restrict__ winkey = nullptr) {
   constexpr bool INLAUNCH = MODE != 0;
   // fp16 stored set (RAW): the wave stages its kept particles' stored values as they are (12 halves, 24 B a
   // row) and the scatter copies them out unchanged, no widening / narrowing (raw_in: the lane's values)
@@ -3340,6 +3347,12 @@ __device__ __forceinline__ void resample_phase(
       int bv = sh.c[0], bi = sh.ci[0];
       for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
       if (lane == 0) cpart[blk] = CountPart{bv, bi};
+      // one-stream k_resample: the block's candidate also goes into the sharded winner keys (max count, then the
+      // lowest index: count in the high word, 2^31 - 1 - index in the low one), so k_resample_final reads
+      // kWinShards keys instead of every block's partial (C4: 39k partials, three round trips)
+      if (winkey && lane == 0 && bv >= 0)
+        __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)), win_key(bv, bi), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       const int loc = bi - blk * kBlock;
       if (!RAW && lane < 12 && bv > 0) ((T*)(cand + blk))[lane] = sh.rows[loc >> 6][loc & 63].q[lane];
       if (stamps && lane == 0) stamp_max(stamps, 5, rt_now());
@@ -3445,7 +3458,7 @@ __device__ __forceinline__ void resample_block(
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
     int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1,
-    LdsConst<T>& sc, OutDev& rec, ResampleLds<T>& sh) {
+    LdsConst<T>& sc, OutDev& rec, ResampleLds<T>& sh, unsigned long long* __restrict__ winkey = nullptr) {
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 4, rt_now());
   const int g = blk / fa.gsz;
   const int n = blk * kBlock + threadIdx.x;
@@ -3498,10 +3511,11 @@ __device__ __forceinline__ void resample_block(
   if (kept)
     resample_phase<T, RNG, MAXM, SP, 0, true>(fa, sc, c, ctrl, table, prior, post, wd, A, A, true, bs, gs, sh, rec, tb,
                                               cand, mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps,
-                                              nullptr, blk, &KR);
+                                              nullptr, blk, &KR, winkey);
   else
     resample_phase<T, RNG, MAXM, SP, 0>(fa, sc, c, ctrl, table, prior, post, wd, A, A, false, bs, gs, sh, rec, tb, cand,
-                                        mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk);
+                                        mlpose, cpart, cgroup, gcount, tcount, counts, out, seq, stamps, nullptr, blk,
+                                        nullptr, winkey);
 }
 
 // Occupancy floor of k_resample / k_resample_multi (waves per SIMD; 1 = the compiler's choice).  Unconstrained
@@ -3522,13 +3536,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? P
     const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan, CountPart* __restrict__ cpart,
     CountPart* __restrict__ cgroup, uint32_t* __restrict__ gcount, uint32_t* __restrict__ tcount,
     uint32_t* __restrict__ counts, Cand* __restrict__ cand, double* __restrict__ mlpose, RecOut* __restrict__ out,
-    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1) {
+    int32_t seq, uint64_t* __restrict__ stamps, const SP* __restrict__ prop0, const SP* __restrict__ prop1,
+    unsigned long long* __restrict__ winkey) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ ResampleLds<T> sh;
   resample_block<T, RNG, MAXM, SP, false, KEPT>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, ctrl,
                                    table, prior, post, w0, w1, bscan0, bscan1, gscan, cpart, cgroup, gcount, tcount,
-                                   counts, cand, mlpose, out, seq, stamps, prop0, prop1, sc, rec, sh);
+                                   counts, cand, mlpose, out, seq, stamps, prop0, prop1, sc, rec, sh, winkey);
 }
 
 template <typename T, int RNG, int MAXM, typename SP, bool KEPT>
@@ -3557,7 +3572,7 @@ __device__ __forceinline__ void resample_final_block(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
     const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
-    int regen, unsigned char* smem /* the blob table */) {
+    int regen, unsigned char* smem /* the blob table */, unsigned long long* __restrict__ winkey = nullptr) {
   __shared__ LdsConst<T> sc;
   __shared__ OutDev rec;
   __shared__ int sv[kFinalBlock / 64], si[kFinalBlock / 64];
@@ -3580,7 +3595,32 @@ __device__ __forceinline__ void resample_final_block(
     for (int q = (int)threadIdx.x; q < n4; q += kFinalBlock) d4[q] = s4[q];
   }
   int bv = -1, bi = 0x7fffffff;
-  {
+  if (winkey) {
+    // one-stream frame: the kWinShards winner keys k_resample's blocks maxed into (one round trip), each reset to
+    // the identity by the thread that read it, for the next frame (the next k_resample is ordered after this
+    // launch).  Key 0 decodes to count 0 at index 2^31 - 1, below every real candidate.
+    static_assert(kWinShards <= kFinalBlock, "one key per thread");
+    unsigned long long key = 0ull;
+    if ((int)threadIdx.x < kWinShards) {
+      key = winkey[threadIdx.x];
+      winkey[threadIdx.x] = 0ull;
+    }
+    unsigned long long kmax = key;
+    // max over the wave of the 64-bit keys (their halves through DPP would need two compares; lane reads are few)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const unsigned long long other = (unsigned long long)__shfl_xor((long long)kmax, o, 64);
+      kmax = other > kmax ? other : kmax;
+    }
+    if (wv == 0 && kmax != 0ull) {
+      bv = (int)(kmax >> 32);
+      bi = 0x7fffffff - (int)(uint32_t)kmax;
+    }
+    if (lane == 0) {
+      sv[wv] = bv;
+      si[wv] = bi;
+    }
+  } else {
     // two partials per 16-B load, eight predicated loads in flight per thread (C4: 39k partials in about
     // three round trips); the buffer holds one spare partial for an odd count (pfmpe_create)
     const int nb = fa.nblk;
@@ -3679,10 +3719,10 @@ __global__ __launch_bounds__(kFinalBlock) void k_resample_final(
     const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, const CountPart* __restrict__ cpart, Cand* __restrict__ cand,
     const double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
-    int regen) {
+    int regen, unsigned long long* __restrict__ winkey) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   resample_final_block<T, RNG, MAXM, SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), ctrl, table, prior,
-                                         cpart, cand, mlpose, out, seq, stamps, regen, smem);
+                                         cpart, cand, mlpose, out, seq, stamps, regen, smem, winkey);
 }
 // batched: block s finishes stream s
 template <typename T, int RNG, int MAXM, typename SP>

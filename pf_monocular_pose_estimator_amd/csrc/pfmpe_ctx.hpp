@@ -76,6 +76,7 @@ struct pfmpe_ctx {
   GroupPart* d_gpart[2] = {nullptr, nullptr};
   GroupScan* d_gscan = nullptr;
   CountPart* d_cpart = nullptr;
+  unsigned long long* d_winkey = nullptr;  // kWinShards winner keys (k_resample -> k_resample_final), zero between frames
   CountPart* d_cgroup = nullptr;
   uint32_t* d_counters = nullptr;  // [prop group x max_grp][prop top][res group x max_grp][res top]
   uint32_t* d_gen = nullptr;       // k_frame iteration release word (monotonic)
@@ -531,11 +532,12 @@ struct Seq {
                          c->d_gscan, c->d_cpart, c->d_cgroup, gcount, tcount,
                          c->record_counts ? c->d_counts : nullptr, c->d_cand, c->d_mlpose, c->d_out, seq,
                          c->d_stamps, kept ? (const SP*)c->d_prop[0] : nullptr,
-                         kept ? (const SP*)c->d_prop[1] : nullptr);
+                         kept ? (const SP*)c->d_prop[1] : nullptr, c->d_winkey);
     }));
     RET(launch_ext(c, PFMPE_K_FINAL, [&] {
       klaunch(c, k_resample_final<T, RNG, MAXM, SP>, dim3(1), dim3(kFinalBlock), BlobTable<T>::bytes(fa.B), fa, c->d_ctrl,
-                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0);
+                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0,
+                         c->d_winkey);
     }));
     RET(wait_frame(c));
     return PFMPE_OK;
@@ -604,6 +606,7 @@ struct Seq {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream));
       if (c->d_flat) HIPCHK(c, hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->flat_base_w = c->flat_base_c = 0;

@@ -88,7 +88,7 @@ size_t build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char
 
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
-                 c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart,
+                 c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart, c->d_winkey,
                  c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps};
   for (void* p : dev)
@@ -234,6 +234,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_gscan, (size_t)c->max_grp * sizeof(GroupScan)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_cpart, (size_t)(c->max_blk + 1) * sizeof(CountPart)) == hipSuccess;  // +1: 16-B reads
   ok &= hipMalloc((void**)&c->d_cgroup, (size_t)c->max_grp * sizeof(CountPart)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_winkey, kWinShards * sizeof(unsigned long long)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_counters, counters_bytes(c)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_gen, sizeof(uint32_t)) == hipSuccess;
@@ -263,6 +264,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok = ok && hipMemsetAsync(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[0], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[1], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
@@ -407,6 +409,7 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
     launch_import<float, float>(c, N, c->anchor[c->prior_idx]);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->N = N;
