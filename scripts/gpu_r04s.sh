@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: after reverting the scalar block-boundary count (it broke the frame shapes' identity, r04r): the shapes'
+# Round 4: the scalar block-boundary count with its sign-extension fix (the bug broke the shapes' identity, r04r): the shapes'
 # records on C5 N=20000 (fused 0 / 1 / 2) first, then the whole -m gpu suite + smoke, then C4 / C5 frames.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out; export TMPDIR=/tmp
