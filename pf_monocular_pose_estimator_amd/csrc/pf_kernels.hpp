@@ -179,6 +179,7 @@ struct alignas(8) CountPart {
 // winner keys of the one-stream two-launch frame (k_resample -> k_resample_final): unsigned max of
 // count << 32 | (2^31 - 1 - index) is the max count at its lowest index; 0 (count 0 at no index) is the identity
 constexpr int kWinShards = 64;
+constexpr int kWinStride = 16;  // keys one 128-B line apart: ~39k block atomics at C4 spread over 64 lines
 __host__ __device__ __forceinline__ unsigned long long win_key(int count, int idx) {
   return ((unsigned long long)(uint32_t)count << 32) | (uint32_t)(0x7fffffff - idx);
 }
@@ -1359,11 +1360,8 @@ __device__ __forceinline__ double div_by_S(double a, double b, double y) {
 // ----------------------------------------------------------------------------- stratified targets
 // r_k = (k + U_k) / N  (PE:671); U_k is the k-th resample draw, taken after all motion draws.
 // fl(k + U_k): the numerator of target r_k = fl(fl(k + U_k) / N)
-// UNI: k is wave-uniform (a block-boundary evaluation); it is moved to an SGPR first, so the generator runs on the
-// scalar unit instead of issuing a whole wave's VALU stream for one lane
-template <typename T, int RNG, bool UNI = false>
+template <typename T, int RNG>
 __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters, int64_t k) {
-  if (UNI) k = (int64_t)(int32_t)__builtin_amdgcn_readfirstlane((uint32_t)k);  // 0 <= k <= N < 2^31
   double U;
   if (RNG == kRngReference) {
     const uint64_t motion = fa.N > 2 ? (uint64_t)12 * (uint64_t)(fa.N - 2) * (uint64_t)iters : 0u;
@@ -1371,8 +1369,7 @@ __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters,
     const uint32_t g2 = lcg_next(g1);
     U = ref_uniform(ref_canonical(g1, g2), 0.0, 1.0);
   } else {
-    const U32x4 o = UNI ? philox4x32_10_uniform((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1)
-                        : philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
+    const U32x4 o = philox4x32_10((uint32_t)k, kTagResample << 24, fa.flo, fa.fhi, fa.key0, fa.key1);
     U = u53(o.x, o.y);
   }
   return (double)(int32_t)k + U;  // 0 <= k <= N < 2^31: one v_cvt_f64_i32 (exact)
@@ -1385,9 +1382,9 @@ __device__ __forceinline__ double target_num(const FrameArgsT<T>& fa, int iters,
 // thr = fl(x*N)*2^-50 + 2^-1000 bounds N*ulp(x) from above with a wide margin (ulp(x) <= x*2^-52 for normal x;
 // the absolute term covers tiny x).  Between the two (a within ~2^-50 relative of x*N) the reference's own
 // division decides.  xn = fl(x*N), thr = fma(xn, 2^-50, 2^-1000): per call site, computed once.
-template <typename T, int RNG, bool UNI = false>
+template <typename T, int RNG>
 __device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, int64_t k, double x, double thr) {
-  const double a = target_num<T, RNG, UNI>(fa, iters, k);
+  const double a = target_num<T, RNG>(fa, iters, k);
   const double Nd = (double)fa.N;
   const double e = __builtin_fma(x, Nd, -a);
   bool le = e >= 0.0;
@@ -1412,7 +1409,7 @@ __device__ __forceinline__ bool target_le(const FrameArgsT<T>& fa, int iters, in
 //   f > k 2^-51.
 // For N < 2^31 both bounds are below kEdge = 1e-6; inside that band (or for x N >= N) the neighbours
 // are scanned explicitly.
-template <typename T, int RNG, bool UNI = false>
+template <typename T, int RNG>
 __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int iters, double x) {
   constexpr double kEdge = 1e-6;
   const int64_t N = fa.N;
@@ -1425,20 +1422,20 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   if (!(fk < (double)N)) {  // x >= ~1: scan down from N
     int64_t k = N;
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && !target_le<T, RNG, UNI>(fa, iters, k - 1, x, thr)) --k;
+    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
     return k;
   }
   int64_t k = (int64_t)(int32_t)fk;  // 0 <= fk < N < 2^31: one v_cvt_i32_f64 (an int64 conversion is five)
   const double f = xn - fk;
-  if (target_le<T, RNG, UNI>(fa, iters, k, x, thr)) {
+  if (target_le<T, RNG>(fa, iters, k, x, thr)) {
     ++k;
     if (1.0 - f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-      while (k < N && target_le<T, RNG, UNI>(fa, iters, k, x, thr)) ++k;
+      while (k < N && target_le<T, RNG>(fa, iters, k, x, thr)) ++k;
     }
   } else if (f <= kEdge) {
 #pragma clang loop unroll(disable) interleave(disable) vectorize(disable)
-    while (k > 0 && !target_le<T, RNG, UNI>(fa, iters, k - 1, x, thr)) --k;
+    while (k > 0 && !target_le<T, RNG>(fa, iters, k - 1, x, thr)) --k;
   }
   return k;
 }
@@ -3196,19 +3193,7 @@ __device__ __forceinline__ void resample_phase(
   if (lane == 63) sh.hi[wv] = hi;
   __syncthreads();
   int lo = wave_shr1(hi, 0);
-  if (wv == 0) {  // the block's first count needs F(rin): block-uniform, so evaluated on the scalar unit (issued as
-                  // a lane-0 VALU stream it cost wave 0 about 150 instructions, ~11 % of the kernel's VALU)
-    // (readfirstlane returns an int: each half goes through uint32_t, or a set bit 31 of the low half would
-    // sign-extend over the high half; that bug, in the first version, made F(rin) 0 for half the blocks)
-    const uint64_t rb = (uint64_t)__double_as_longlong(rin);
-    const uint64_t rlo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)rb);
-    const uint64_t rhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(rb >> 32));
-    const double ru = __longlong_as_double((long long)(rlo | (rhi << 32)));
-    const int lo0 = (int)count_targets<T, RNG, true>(fa, __builtin_amdgcn_readfirstlane(iters), ru);
-    if (lane == 0) lo = lo0;
-  } else if (lane == 0) {
-    lo = sh.hi[wv - 1];
-  }
+  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : sh.hi[wv - 1];
   const int cntn = valid ? hi - lo : 0;
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 11, rt_now());
   if (counts && valid) counts[n] = (uint32_t)cntn;
@@ -3354,7 +3339,7 @@ __device__ __forceinline__ void resample_phase(
       // lowest index: count in the high word, 2^31 - 1 - index in the low one), so k_resample_final reads
       // kWinShards keys instead of every block's partial (C4: 39k partials, three round trips)
       if (winkey && lane == 0 && bv >= 0)
-        __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)), win_key(bv, bi), __ATOMIC_RELAXED,
+        __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, win_key(bv, bi), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
       const int loc = bi - blk * kBlock;
       if (!RAW && lane < 12 && bv > 0) ((T*)(cand + blk))[lane] = sh.rows[loc >> 6][loc & 63].q[lane];
@@ -3605,8 +3590,8 @@ __device__ __forceinline__ void resample_final_block(
     static_assert(kWinShards <= kFinalBlock, "one key per thread");
     unsigned long long key = 0ull;
     if ((int)threadIdx.x < kWinShards) {
-      key = winkey[threadIdx.x];
-      winkey[threadIdx.x] = 0ull;
+      key = winkey[threadIdx.x * kWinStride];
+      winkey[threadIdx.x * kWinStride] = 0ull;
     }
     unsigned long long kmax = key;
     // max over the wave of the 64-bit keys (their halves through DPP would need two compares; lane reads are few)

@@ -118,26 +118,6 @@ PF_HD U32x4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, ui
   return U32x4{c0, c1, c2, c3};
 }
 
-// The same generator for a wave-uniform counter (all six words in SGPRs): plain xors, so every round stays on
-// the scalar unit (s_mul_hi_u32 / s_mul_i32 / s_xor_b32) instead of a wave-wide VALU stream for one value.
-PF_HD U32x4 philox4x32_10_uniform(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int r = 0; r < 10; ++r) {
-    if (r) {
-      k0 += 0x9E3779B9u;
-      k1 += 0xBB67AE85u;
-    }
-    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-    const uint32_t n1 = (uint32_t)p1;
-    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-    const uint32_t n3 = (uint32_t)p0;
-    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-  }
-  return U32x4{c0, c1, c2, c3};
-}
-
 // 24-bit uniform in [0,1): exactly representable in float and double
 PF_HD float u24f(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
 PF_HD double u24d(uint32_t x) { return (double)(x >> 8) * (1.0 / 16777216.0); }

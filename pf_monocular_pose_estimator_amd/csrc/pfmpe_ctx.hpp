@@ -606,7 +606,7 @@ struct Seq {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
       HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
-      HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream));
       if (c->d_flat) HIPCHK(c, hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream));
       HIPCHK(c, hipStreamSynchronize(c->stream));
       c->flat_base_w = c->flat_base_c = 0;

@@ -234,7 +234,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_gscan, (size_t)c->max_grp * sizeof(GroupScan)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_cpart, (size_t)(c->max_blk + 1) * sizeof(CountPart)) == hipSuccess;  // +1: 16-B reads
   ok &= hipMalloc((void**)&c->d_cgroup, (size_t)c->max_grp * sizeof(CountPart)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_winkey, kWinShards * sizeof(unsigned long long)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_winkey, kWinShards * kWinStride * sizeof(unsigned long long)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_counters, counters_bytes(c)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_gen, sizeof(uint32_t)) == hipSuccess;
@@ -264,7 +264,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok = ok && hipMemsetAsync(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream) == hipSuccess;
-  ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[0], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[1], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
@@ -409,7 +409,7 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
     launch_import<float, float>(c, N, c->anchor[c->prior_idx]);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->N = N;
