@@ -1440,6 +1440,34 @@ __device__ __forceinline__ int64_t count_targets(const FrameArgsT<T>& fa, int it
   return k;
 }
 
+// count_targets for a whole wave, the common case straight-line: with x in [0, ~1), xn = x N away from an integer
+// by more than kEdge on both sides, ONE target evaluation k = floor(xn) decides F(x) = k + [r_k <= x] (count_targets'
+// argument), and outside the 2^-50 band its sign test needs no division.  Lanes that are not in that case (x < 0
+// or NaN, x N >= N, near an integer, in the band) redo count_targets itself behind a wave-uniform test.  Without
+// the exec-mask branches of count_targets' rare paths the common path is one basic block (k_resample: fewer SALU
+// and VALU per wave).  Same result as count_targets for every active lane.
+template <typename T, int RNG>
+__device__ __forceinline__ int count_targets_wave(const FrameArgsT<T>& fa, int iters, double x, bool active) {
+  constexpr double kEdge = 1e-6;  // count_targets' band around integers
+  const double Nd = (double)fa.N;
+  const double xn = x * Nd;
+  const double fk = floor(xn);
+  const double f = xn - fk;
+  const bool simple = x >= 0.0 && fk < Nd && f > kEdge && 1.0 - f > kEdge;
+  const int k = simple ? (int)fk : 0;
+  const double a = target_num<T, RNG>(fa, iters, k);
+  const double e = __builtin_fma(x, Nd, -a);
+  const double thr = __builtin_fma(xn, 0x1p-50, 0x1p-1000);
+  const bool le = e >= 0.0;
+  const bool band = !le && !(-e > thr);
+  int res = k + (le ? 1 : 0);
+  const bool slow = active && (!simple || band);
+  if (__builtin_amdgcn_ballot_w64(slow)) {
+    if (slow) res = (int)count_targets<T, RNG>(fa, iters, x);
+  }
+  return res;
+}
+
 // ----------------------------------------------------------------------------- in-launch hand-off
 // Per-block / per-group partials go to the last arriver (MI355X_MICROARCH.md "Valid forms", row 1):
 // every partial word is stored write-through (sc1, agent scope) by the one lane that then drains
@@ -3189,7 +3217,8 @@ __device__ __forceinline__ void resample_phase(
 #pragma clang loop unroll(disable)
   for (int w = 0; w < wvu; ++w) pm = sh.max[w] > pm ? sh.max[w] : pm;
   const double R = rm > pm ? rm : pm;
-  const int hi = valid ? (int)count_targets<T, RNG>(fa, iters, R) : N;
+  int hi = count_targets_wave<T, RNG>(fa, iters, R, valid);  // every lane (one basic block); invalid lanes:
+  hi = valid ? hi : N;                                         // their R is the wave's last, the result unused
   if (lane == 63) sh.hi[wv] = hi;
   __syncthreads();
   int lo = wave_shr1(hi, 0);
