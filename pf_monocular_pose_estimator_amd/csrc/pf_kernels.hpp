@@ -3222,7 +3222,13 @@ __device__ __forceinline__ void resample_phase(
   if (lane == 63) sh.hi[wv] = hi;
   __syncthreads();
   int lo = wave_shr1(hi, 0);
-  if (lane == 0) lo = (wv == 0) ? (int)count_targets<T, RNG>(fa, iters, rin) : sh.hi[wv - 1];
+  if (wv == 0) {  // F(rin), block-uniform: every lane of wave 0 takes the straight-line common case together (rin is
+                  // the same in every lane), only lane 0 the rare paths
+    const int lo0 = count_targets_wave<T, RNG>(fa, iters, rin, lane == 0);
+    if (lane == 0) lo = lo0;
+  } else if (lane == 0) {
+    lo = sh.hi[wv - 1];
+  }
   const int cntn = valid ? hi - lo : 0;
   if (stamps && threadIdx.x == 0) stamp_max(stamps, 11, rt_now());
   if (counts && valid) counts[n] = (uint32_t)cntn;
