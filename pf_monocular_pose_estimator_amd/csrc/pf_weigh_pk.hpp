@@ -477,17 +477,24 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
       u[j] = su * rz;
       v[j] = sv * rz;
     }
-    // ---- column minima over the 2D grid (column_minima's grid branch), both particles
+    // ---- column minima over the 2D grid (column_minima's grid branch), both particles.  In phases over the
+    // markers (every cell record, then every first entry, then the rare longer lists behind one test): a
+    // per-marker branch kept each marker's two dependent LDS round trips from overlapping the next marker's
     float mA[MAXM], mB[MAXM];
     int rA[MAXM], rB[MAXM];
+    uint32_t recA[MAXM], recB[MAXM];
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
       const f32x2 fx = pk_fma(u[j], pk_splat(pl.inv_c), pk_splat(pl.ox));
       const f32x2 fy = pk_fma(v[j], pk_splat(pl.inv_c), pk_splat(pl.oy));
-      const uint32_t recA = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.x, fy.x);
-      const uint32_t recB = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.y, fy.y);
-      const GridEnt eA = *(const GridEnt*)(ents + (recA & 0xffffu));
-      const GridEnt eB = *(const GridEnt*)(ents + (recB & 0xffffu));
+      recA[j] = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.x, fy.x);
+      recB[j] = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.y, fy.y);
+    }
+    uint32_t lists = 0;  // a record above 0x1ffff: a list longer than one
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) {
+      const GridEnt eA = *(const GridEnt*)(ents + (recA[j] & 0xffffu));
+      const GridEnt eB = *(const GridEnt*)(ents + (recB[j] & 0xffffu));
       const f32x2 dx = f32x2{eA.x, eB.x} - u[j];
       const f32x2 dy = f32x2{eA.y, eB.y} - v[j];
       const f32x2 dd = pk_fma(dx, dx, dy * dy);
@@ -495,10 +502,15 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
       mB[j] = dd.y;
       rA[j] = eA.orig;
       rB[j] = eB.orig;
-      if (__builtin_amdgcn_ballot_w64((recA > 0x1ffffu) | (recB > 0x1ffffu))) {  // a list longer than one
-        grid_walk(ents, recA, u[j].x, v[j].x, mA[j], rA[j]);
-        grid_walk(ents, recB, u[j].y, v[j].y, mB[j], rB[j]);
-      }
+      lists |= recA[j] | recB[j];
+    }
+    if (__builtin_amdgcn_ballot_w64(lists > 0x1ffffu)) {  // rare (wave-uniform)
+#pragma unroll
+      for (int j = 0; j < MAXM; ++j)
+        if (__builtin_amdgcn_ballot_w64((recA[j] > 0x1ffffu) | (recB[j] > 0x1ffffu))) {
+          grid_walk(ents, recA[j], u[j].x, v[j].x, mA[j], rA[j]);
+          grid_walk(ents, recB[j], u[j].y, v[j].y, mB[j], rB[j]);
+        }
     }
     // ---- score (score_unordered: B >= M, the host checks), both particles
     f32x2 Pr = pk_splat(0.0f);
