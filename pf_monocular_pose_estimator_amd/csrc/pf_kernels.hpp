@@ -798,7 +798,9 @@ __device__ __forceinline__ int bucket_of_bf(float x, float xmin, float inv_bw, i
   return (int)__builtin_fminf(__builtin_fmaxf(f, 0.0f), (float)(nb - 1));
 }
 
-template <typename T, int MAXM, bool PRUNE>
+// PHASED (k_frame2, whose VGPR budget holds every marker's cell record): the grid branch in phases over the
+// markers; the register-capped streaming kernels keep the per-marker form (the phases spill there)
+template <typename T, int MAXM, bool PRUNE, bool PHASED = false>
 __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u, const T* v,
                                              const LdsBlobs<T>& tb, T* m, int* r) {
   const int B = fa.B, M = fa.M;
@@ -831,51 +833,129 @@ __device__ __forceinline__ int column_minima(const FrameArgsT<T>& fa, const T* u
       const unsigned char* cells = tb.base + ga.cell_off;
       const unsigned char* ents = tb.base + ga.ent_off;
       const f32x2 ic = pk2(ga.inv_c, ga.inv_c), oc = pk2(ga.ox, ga.oy);
-#pragma unroll
-      for (int j = 0; j < MAXM; ++j) {
-        float bd = INFINITY;
-        int bo = 0;
-        if (marker_live<MAXM>(j, M)) {
-          const f32x2 uvj = pk2(u[j], v[j]);
-          const f32x2 f = pk_fma(uvj, ic, oc);  // both cell coordinates in one v_pk_fma_f32
-          const int cx = (int)__builtin_amdgcn_fmed3f(f.x, 0.0f, ga.fmaxx);
-          const int cy = (int)__builtin_amdgcn_fmed3f(f.y, 0.0f, ga.fmaxy);
-          // byte offset cy * 4 ncx + 4 cx (the row pitch scaled on the host)
-          const uint32_t rec = *(const uint32_t*)(cells + mad24(cy, ga.ncx4, cx << 2));
-          const GridEnt* e = (const GridEnt*)(ents + (rec & 0xffffu));
-          const int n = (int)(rec >> 16);
-          visited += n;
-          auto visit = [&](const GridEnt& ec, bool in) {
-            const f32x2 dd = pk2(ec.x, ec.y) - uvj;
-            const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
-            const bool take = in & (d < bd);
-            bd = take ? d : bd;
-            bo = take ? ec.orig : bo;
-          };
-          // The 12 / 16-marker buckets (C3: 200 blobs, clustered, most lists longer than one) read the first
-          // two entries together; the exact 5-marker bucket (50 blobs) reads one and walks further entries only
-          // when some lane of the wave needs them.
-          constexpr int c1 = MAXM > kExactM ? 2 : 1;
-          {
+      if constexpr (PHASED) {
+        // In phases over the markers (every cell record, then every first entry, then the longer lists behind
+        // one wave-uniform test): a per-marker branch kept each marker's two dependent LDS round trips from
+        // overlapping the next marker's, and at C2 (1.5 waves per SIMD) nothing else hides them
+        uint32_t rec[MAXM];
+  #pragma unroll
+        for (int j = 0; j < MAXM; ++j) {
+          rec[j] = 0;
+          if (marker_live<MAXM>(j, M)) {
+            const f32x2 f = pk_fma(pk2(u[j], v[j]), ic, oc);  // both cell coordinates in one v_pk_fma_f32
+            const int cx = (int)__builtin_amdgcn_fmed3f(f.x, 0.0f, ga.fmaxx);
+            const int cy = (int)__builtin_amdgcn_fmed3f(f.y, 0.0f, ga.fmaxy);
+            // byte offset cy * 4 ncx + 4 cx (the row pitch scaled on the host)
+            rec[j] = *(const uint32_t*)(cells + mad24(cy, ga.ncx4, cx << 2));
+          }
+        }
+        // The 12 / 16-marker buckets (C3: 200 blobs, clustered, most lists longer than one) read the first two
+        // entries together; the exact 5-marker bucket (50 blobs) reads one and walks further entries only when
+        // some lane of the wave needs them.
+        constexpr int c1 = MAXM > kExactM ? 2 : 1;
+        bool more = false;  // some live marker's list has more than c1 entries
+  #pragma unroll
+        for (int j = 0; j < MAXM; ++j) {
+          float bd = INFINITY;
+          int bo = 0;
+          if (marker_live<MAXM>(j, M)) {
+            const f32x2 uvj = pk2(u[j], v[j]);
+            const GridEnt* e = (const GridEnt*)(ents + (rec[j] & 0xffffu));
+            const int n = (int)(rec[j] >> 16);
+            visited += n;
+            more |= n > c1;
             const GridEnt e0 = e[0];
             const f32x2 dd = pk2(e0.x, e0.y) - uvj;  // (dx, dy) in one v_pk_add_f32
             bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
             bo = e0.orig;
-            if constexpr (c1 == 2) visit(e[1], n > 1);
+            if constexpr (c1 == 2) {
+              const GridEnt e1 = e[1];
+              const f32x2 d1 = pk2(e1.x, e1.y) - uvj;
+              const float d = fmadd(d1.x, d1.x, d1.y * d1.y);
+              const bool take = (n > 1) & (d < bd);
+              bd = take ? d : bd;
+              bo = take ? e1.orig : bo;
+            }
           }
-          if (__builtin_amdgcn_ballot_w64(n > c1)) {  // some lane's list has more entries (rare at 50 blobs)
+          m[j] = bd;
+          r[j] = bo;
+        }
+        if (__builtin_amdgcn_ballot_w64(more)) {  // rare at 50 blobs
+  #pragma unroll
+          for (int j = 0; j < MAXM; ++j) {
+            if (!marker_live<MAXM>(j, M)) continue;
+            const int n = (int)(rec[j] >> 16);
+            if (!__builtin_amdgcn_ballot_w64(n > c1)) continue;
+            const f32x2 uvj = pk2(u[j], v[j]);
+            const GridEnt* e = (const GridEnt*)(ents + (rec[j] & 0xffffu));
+            float bd = m[j];
+            int bo = r[j];
+            auto visit = [&](const GridEnt& ec, bool in) {
+              const f32x2 dd = pk2(ec.x, ec.y) - uvj;
+              const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
+              const bool take = in & (d < bd);
+              bd = take ? d : bd;
+              bo = take ? ec.orig : bo;
+            };
             // two entries per step, the second masked past the list end (its LDS read stays inside the table
             // or its 16-B tail granule, BlobTable::lds_bytes)
-#pragma unroll 2
+  #pragma unroll 2
             for (int c = c1; c < n; c += 2) {
               const GridEnt ea = e[c], eb = e[c + 1];
               visit(ea, true);
               visit(eb, c + 1 < n);
             }
+            m[j] = bd;
+            r[j] = bo;
           }
         }
-        m[j] = bd;
-        r[j] = bo;
+      } else {
+  #pragma unroll
+        for (int j = 0; j < MAXM; ++j) {
+          float bd = INFINITY;
+          int bo = 0;
+          if (marker_live<MAXM>(j, M)) {
+            const f32x2 uvj = pk2(u[j], v[j]);
+            const f32x2 f = pk_fma(uvj, ic, oc);  // both cell coordinates in one v_pk_fma_f32
+            const int cx = (int)__builtin_amdgcn_fmed3f(f.x, 0.0f, ga.fmaxx);
+            const int cy = (int)__builtin_amdgcn_fmed3f(f.y, 0.0f, ga.fmaxy);
+            // byte offset cy * 4 ncx + 4 cx (the row pitch scaled on the host)
+            const uint32_t rec = *(const uint32_t*)(cells + mad24(cy, ga.ncx4, cx << 2));
+            const GridEnt* e = (const GridEnt*)(ents + (rec & 0xffffu));
+            const int n = (int)(rec >> 16);
+            visited += n;
+            auto visit = [&](const GridEnt& ec, bool in) {
+              const f32x2 dd = pk2(ec.x, ec.y) - uvj;
+              const float d = fmadd(dd.x, dd.x, dd.y * dd.y);
+              const bool take = in & (d < bd);
+              bd = take ? d : bd;
+              bo = take ? ec.orig : bo;
+            };
+            // The 12 / 16-marker buckets (C3: 200 blobs, clustered, most lists longer than one) read the first
+            // two entries together; the exact 5-marker bucket (50 blobs) reads one and walks further entries only
+            // when some lane of the wave needs them.
+            constexpr int c1 = MAXM > kExactM ? 2 : 1;
+            {
+              const GridEnt e0 = e[0];
+              const f32x2 dd = pk2(e0.x, e0.y) - uvj;  // (dx, dy) in one v_pk_add_f32
+              bd = __builtin_fminf(fmadd(dd.x, dd.x, dd.y * dd.y), INFINITY);
+              bo = e0.orig;
+              if constexpr (c1 == 2) visit(e[1], n > 1);
+            }
+            if (__builtin_amdgcn_ballot_w64(n > c1)) {  // some lane's list has more entries (rare at 50 blobs)
+              // two entries per step, the second masked past the list end (its LDS read stays inside the table
+              // or its 16-B tail granule, BlobTable::lds_bytes)
+  #pragma unroll 2
+              for (int c = c1; c < n; c += 2) {
+                const GridEnt ea = e[c], eb = e[c + 1];
+                visit(ea, true);
+                visit(eb, c + 1 < n);
+              }
+            }
+          }
+          m[j] = bd;
+          r[j] = bo;
+        }
       }
       return visited;
     }
@@ -2140,7 +2220,7 @@ __device__ __forceinline__ void propagate_top(const FrameArgsT<T>& fa, Ctrl* __r
 }
 
 // ---- one particle through the motion model, projection and likelihood (PE:543-604, PE:2385)
-template <typename T, int RNG, int MAXM, bool PRUNE>
+template <typename T, int RNG, int MAXM, bool PRUNE, bool PHASED = false>
 __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
                                             const T* A, int n, int iter, T* P, int* nvisit = nullptr,
                                             uint64_t* st = nullptr) {
@@ -2153,7 +2233,7 @@ __device__ __forceinline__ T weigh_particle(const FrameArgsT<T>& fa, const LdsCo
   if (fa.B > 0 && !nan_at_origin_tb(fa, tb, u[0], v[0])) {
     T m[MAXM];
     int r[MAXM];
-    const int visited = column_minima<T, MAXM, PRUNE>(fa, u, v, tb, m, r);
+    const int visited = column_minima<T, MAXM, PRUNE, PHASED>(fa, u, v, tb, m, r);
     if (nvisit) *nvisit = visited;
     if (st && threadIdx.x == 0) stamp_max(st, 29, rt_now() + (m[0] == (T)12345 ? 1 : 0));
     if constexpr (std::is_same<T, float>::value) {
@@ -4112,7 +4192,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   for (;; ++iter) {
     const int slot = c.cur_slot;
     if (valid) {
-      w = weigh_particle<T, RNG, MAXM, PRUNE>(fa, sc, tb, A, n, iter, P, nullptr, stamps);
+      w = weigh_particle<T, RNG, MAXM, PRUNE, true>(fa, sc, tb, A, n, iter, P, nullptr, stamps);
       (slot ? w1 : w0)[n] = w;
     }
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 9, rt_now());
