@@ -199,8 +199,17 @@ def cpu_multiprocess(procs: int, n_frames: int):
     updates/s = sum over processes of (updates / own PF-block time)."""
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs) as pool:
+    # close + join, not the context manager's terminate(): a SIGTERM'd worker prints an "Aborted" dump into
+    # every profiler log (VERDICT r04 weak 7)
+    pool = ctx.Pool(procs)
+    try:
         res = pool.starmap(_c1_stream_rate, [(100 + i, n_frames) for i in range(procs)])
+        pool.close()
+    except BaseException:
+        pool.terminate()
+        raise
+    finally:
+        pool.join()
     return {"procs": procs, "value": sum(u / t for _, u, t in res), "unit": "particle-updates/s",
             "sample": f"C1 x {procs} independent streams, {n_frames} frames each after 5 warm-up, one process each"}
 

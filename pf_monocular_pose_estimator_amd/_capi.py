@@ -24,7 +24,7 @@ OPT_RECORD_COUNTS, OPT_PRUNE, OPT_TIMING, OPT_FUSED, OPT_KEEP_PROPAGATED = 1, 2,
 OPT_WAIT_BOUND_US, OPT_FUSED_REARM, OPT_MULTI_MAX_BLOCKS = 6, 7, 8
 OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
 DIAG_LAG_LOADS, DIAG_ABANDON, DIAG_NO_STREAM, DIAG_FORCE_STREAM, DIAG_SERIAL_TOP = 64, 128, 512, 1024, 2048
-DIAG_NO_PK, DIAG_CORRUPT_DESC, DIAG_NO_DEFER = 4096, 8192, 16384
+DIAG_NO_PK, DIAG_CORRUPT_DESC, DIAG_NO_DEFER, DIAG_BLOCK_RESAMPLE = 4096, 8192, 16384, 32768
 OPT_DEFER_RESAMPLE = 9
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
 INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N, INFO_LAST_WEIGH_PASS = 1, 2, 3, 4, 5, 6
@@ -320,8 +320,8 @@ class Engine:
         return out
 
     def step_batch(self, frames) -> list:
-        """Frames (a list of FrameIn) run back to back in C, each blocking on its own record."""
-        return self.run_batch(self.prepare_batch(frames))
+        """Frames (a list of FrameIn) run back to back in C, each blocking on its own record; returns a list."""
+        return list(self.run_batch(self.prepare_batch(frames)))
 
     @staticmethod
     def prepare_batch(frames):
@@ -330,8 +330,10 @@ class Engine:
         n = len(frames)
         return n, (FrameIn * n)(*frames), (FrameOut * n)()
 
-    def run_batch(self, prepared) -> list:
-        """pfmpe_step_batch over prepare_batch's arrays; returns the outputs (the ctypes array's elements)."""
+    def run_batch(self, prepared):
+        """pfmpe_step_batch over prepare_batch's arrays; returns prepare_batch's output array itself (a ctypes
+        FrameOut array, not a copy): a second run over the same prepared arrays overwrites it (the bench's timed loop
+        reuses them on purpose)."""
         n, arr_in, arr_out = prepared
         done = C.c_int()
         self._chk(self.lib.pfmpe_step_batch(self.ctx, arr_in, n, arr_out, C.byref(done)))

@@ -1632,7 +1632,9 @@ enum : int {
   kDiagNoPk = 4096,        // two-launch path: never the two-particles-per-lane pass k_weigh_pk (A/B, tests)
   kDiagCorruptDesc = 8192, // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
                            // staging check; the altered word is a key word, never a pointer)
-  kDiagNoDefer = 16384     // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
+  kDiagNoDefer = 16384,    // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
+  kDiagBlockResample = 32768  // deferred two-launch frames resample with the block-per-256 k_resample instead of
+                              // k_resample_owners' wave per 256 (A/B, identity tests)
 };
 __device__ __forceinline__ uint64_t rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 // per-block stamps go to the block's own row (plain stores, no contended atomics); the host reduces rows
@@ -3664,6 +3666,261 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? P
                                    d.prior, d.post, d.w0, d.w1, d.bscan0, d.bscan1, d.gscan, d.cpart, d.cgroup,
                                    d.gcount_r, d.tcount_r, d.counts, d.cand, d.mlpose, d.out, d.seq, nullptr, d.prop0,
                                    d.prop1, sc, rec, sh);
+}
+
+// ---- launch 2 of a deferred two-launch frame: stratified resampling of ONE 256-particle block
+// by ONE wave.  The frame has the kept propagated set and defers the new prior (fa.owner_out), so a block's work is
+// its scan, its target counts, its owner indices and its winner key: nothing that needs the block's other waves.
+// Lane l handles the block's particles l, 64 + l, 128 + l, 192 + l ("chunks" c = 0..3, exactly the four waves of
+// resample_phase), so every scan keeps resample_phase's association: the chunk's DPP scan, then the earlier chunks'
+// totals added in chunk order (block_incl_from_wave's `pre`), the running maximum carried from chunk to chunk in
+// the order of its `pm` loop, and the lower target count of lane 0 taken from the previous chunk's lane 63 (the
+// `sh.hi` hand-off) or, for chunk 0, F(rin).  The wave-uniform shortcuts (fixed-point scan, division by
+// reciprocal, monotone running max, integer winner keys) are each decided once for the four chunks; every one of
+// them yields the same bits as its general form wherever it is taken, so the decision granularity does not change
+// any output.  Outputs are resample_phase's for MODE 0 with owner_out: owner_out, counts, the winner key and the
+// most-likely pose (k_resample_final reads the keys, not the count partials, which are therefore not written).
+// No workgroup barrier: the per-wave scalar work (control record, scan words, key schedule, loop control) is paid
+// once per 256 particles instead of once per 64, and a wave never waits for the other three.
+template <typename T>
+struct OwnersLds {
+  LdsConst<T> sc;  // the frame constants, staged only by the wave holding the most-likely particle
+};
+template <typename T, int RNG, typename SP>
+__device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk,
+                                                     const Ctrl& c, const SP* __restrict__ prior,
+                                                     const T* __restrict__ w0, const T* __restrict__ w1,
+                                                     const BlockScan& bs, const GroupScan& gs,
+                                                     uint32_t* __restrict__ counts, double* __restrict__ mlpose,
+                                                     unsigned long long* __restrict__ winkey, OwnersLds<T>& sh,
+                                                     int wv, const T (&wa)[4], const T (&wb)[4]) {
+  constexpr int kC = kBlock / 64;
+  const int N = fa.N;
+  const int lane = lane_id();
+  const int base_n = blk * kBlock;
+  const int iters = c.iters;
+  const double S = c.S;
+  const int64_t Kt = c.K_total;
+  const int slot = c.kept_slot;
+  bool valid[kC];
+  double wd[kC];
+  bool out_fx = false, out_neg = false;
+#pragma unroll
+  for (int q = 0; q < kC; ++q) {
+    valid[q] = base_n + q * 64 + lane < N;
+    wd[q] = valid[q] ? (double)(slot ? wb[q] : wa[q]) : 0.0;
+    out_fx |= valid[q] && !(wd[q] >= 0.0 && wd[q] < 32.0);
+    out_neg |= valid[q] && wd[q] < 0.0;
+  }
+  // resample_phase's per-wave choices, taken for the four chunks at once (same bits either way, see above)
+  const bool fx = std::is_same<T, float>::value && fa.M >= 4 && __ballot(out_fx) == 0;
+  const bool nonneg = fx || __ballot(out_neg) == 0;
+  const bool recip = std::is_same<T, float>::value && nonneg && S > 0x1p-1000 && S < 0x1p1000;
+  // running max at the block start (resample_phase's rin)
+  double rin = gs.Gin;
+  if ((blk % fa.gsz) != 0) {
+    const double zin = S > 0.0 ? bs.zin_max : bs.zin_min;
+    const double zn = gs.G + zin;
+    const double cz = recip && zn >= 0.0 && zn <= 2.0 * S ? div_by_S(zn, S, c.invS) : zn / S;
+    rin = cz > rin ? cz : rin;
+  }
+  // F(rin): every lane takes the straight-line common case together, lane 0 alone the rare paths
+  int prev_hi = lane_value(count_targets_wave<T, RNG>(fa, iters, rin, lane == 0), 0);
+  double pre = 0.0;  // the earlier chunks' totals, summed in chunk order
+  double pm = rin;   // the running max over rin and the earlier chunks
+  int ra[kC], re[kC], rc[kC];
+  int kmax = -1;  // max of count * 256 + (255 - particle in block): the max count at its lowest index
+  int cmax = -1;  // the lane's largest count
+#pragma unroll
+  for (int q = 0; q < kC; ++q) {
+    const double wi = fx ? wave_incl_sum_fx((float)wd[q]) : wave_incl_sum(wd[q]);
+    const double incl = pre + wi;
+    pre = pre + lane_value(wi, 63);
+    const double num = gs.G + (bs.E + incl);
+    const double cn = recip ? div_by_S(num, S, c.invS) : num / S;
+    double rm;
+    if (S > 0.0 && nonneg) {  // c is non-decreasing over the chunk's valid lanes: its running max is c itself
+      const uint64_t vmask = __ballot(valid[q]);
+      const double last = vmask ? lane_value(cn, 63 - __builtin_clzll(vmask)) : -INFINITY;
+      rm = valid[q] ? cn : last;
+    } else {
+      rm = wave_incl_max(valid[q] ? cn : -INFINITY);
+    }
+    const double R = rm > pm ? rm : pm;
+    const double mq = lane_value(rm, 63);
+    pm = mq > pm ? mq : pm;
+    int hi = count_targets_wave<T, RNG>(fa, iters, R, valid[q]);
+    hi = valid[q] ? hi : N;
+    int lo = wave_shr1(hi, 0);
+    if (lane == 0) lo = prev_hi;
+    prev_hi = lane_value(hi, 63);
+    const int cntn = valid[q] ? hi - lo : 0;
+    const int n = base_n + q * 64 + lane;
+    if (counts && valid[q]) counts[n] = (uint32_t)cntn;
+    // write range [a, e) (resample_phase: targets past K_total copy the last found particle, PE:681)
+    int a, e;
+    if (!valid[q]) {
+      a = e = N;
+    } else if (Kt == 0) {
+      a = 0;
+      e = (n == N - 1) ? N : 0;
+    } else if (lo >= Kt) {
+      a = e = N;
+    } else if (hi == Kt) {
+      a = lo;
+      e = N;
+    } else {
+      a = lo;
+      e = hi;
+    }
+    ra[q] = a;
+    re[q] = e;
+    rc[q] = valid[q] ? cntn : -1;
+    kmax = max(kmax, valid[q] ? cntn * 256 + (255 - (q * 64 + lane)) : -1);  // (unused if a count is >= 2^23)
+    cmax = max(cmax, rc[q]);
+  }
+  // block max count, first index (the winner candidate): one integer key unless some count is >= 2^23 (always below
+  // at N < 2^23; at larger N all but degenerate frames)
+  int bv, bi;
+  if (N < (1 << 23) || __ballot(cmax >= (1 << 23)) == 0) {
+    int k = kmax;
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor1, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppQuadXor2, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowHalfMirror, 0xf, 0xf, true));
+    k = max(k, __builtin_amdgcn_mov_dpp(k, kDppRowMirror, 0xf, 0xf, true));
+    k = max(k, dpp<kDppBcast15, 0xa>(k, INT_MIN));
+    k = max(k, dpp<kDppBcast31, 0xc>(k, INT_MIN));
+    k = __builtin_amdgcn_readlane(k, 63);
+    bv = k < 0 ? -1 : k >> 8;
+    bi = k < 0 ? 0x7fffffff : base_n + 255 - (k & 255);
+  } else {
+    bv = -1;
+    bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < kC; ++q) cmb_max(bv, bi, rc[q], rc[q] >= 0 ? base_n + q * 64 + lane : 0x7fffffff);
+    wave_argmax(bv, bi);
+  }
+
+  // the most likely pose for the frame record (write-through), regenerated by its lane (the kept set holds stored
+  // state values, not poses); the frame constants are staged by this one wave (wave-uniform test)
+  const int mli = c.most_likely_idx;
+  if (mli >= base_n && mli < base_n + kBlock && mli < N) {
+    uint32_t* dst = (uint32_t*)&sh.sc;
+    constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
+    for (int i = lane; i < kWordsC; i += 64) dst[i] = fa_words[i];
+    wave_lds_sync();
+    if (lane == ((mli - base_n) & 63)) {
+      T Q[12];
+      make_particle<T, RNG, SP>(fa, sh.sc, prior, mli, c.kept_iter, Q);
+#pragma unroll
+      for (int q = 0; q < 12; ++q) st_wt_d(mlpose + q, (double)Q[q]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+
+  // Owner indices: particle p of the block owns the slots [ra, re) of its lane and chunk (consecutive, non-empty
+  // ranges in particle order).  Each lane writes its own particles' ranges: first 16-B stores of four slots while at
+  // least four remain, then single slots; a store past its range goes to an offset the buffer's range check drops
+  // (no exec-mask branches).  In a typical frame every range is a few slots and the lanes' ranges are adjacent, so a
+  // round's stores fall on a few consecutive lines; where the weight concentrates (ranges of tens of slots in a whole
+  // region of the set) the 16-B stores quarter the write transactions.  A range longer than kWide (one particle
+  // taking a large share of the targets) is written by the whole wave, 64 consecutive slots per store, one such
+  // particle after another.
+  constexpr int kWide = 256;
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)fa.owner_out, (short)0, (int)(N * 4),
+                                                                          0x00020000);
+  constexpr uint32_t kDrop = 0x80000000u;  // past num_records: the store is dropped
+  int m4 = 0, m1 = 0;
+  bool wide = false;
+#pragma unroll
+  for (int q = 0; q < kC; ++q) {
+    const int len = re[q] - ra[q];
+    m4 = max(m4, len <= kWide ? len >> 2 : 0);
+    m1 = max(m1, len <= kWide ? len & 3 : 0);
+    wide |= len > kWide;
+  }
+  m4 = max(m4, __builtin_amdgcn_mov_dpp(m4, kDppQuadXor1, 0xf, 0xf, true));
+  m4 = max(m4, __builtin_amdgcn_mov_dpp(m4, kDppQuadXor2, 0xf, 0xf, true));
+  m4 = max(m4, __builtin_amdgcn_mov_dpp(m4, kDppRowHalfMirror, 0xf, 0xf, true));
+  m4 = max(m4, __builtin_amdgcn_mov_dpp(m4, kDppRowMirror, 0xf, 0xf, true));
+  m4 = max(m4, dpp<kDppBcast15, 0xa>(m4, 0));
+  m4 = max(m4, dpp<kDppBcast31, 0xc>(m4, 0));
+  m4 = __builtin_amdgcn_readlane(m4, 63);
+  // the largest remainder (<= 3) by ballots
+  m1 = __builtin_amdgcn_ballot_w64(m1 >= 3) ? 3 : __builtin_amdgcn_ballot_w64(m1 >= 2) ? 2
+                                                : __builtin_amdgcn_ballot_w64(m1 >= 1) ? 1 : 0;
+  for (int j = 0; j < m4; ++j) {
+#pragma unroll
+    for (int q = 0; q < kC; ++q) {
+      const int len = re[q] - ra[q];
+      const uint32_t off = len <= kWide && 4 * j + 4 <= len ? (uint32_t)(ra[q] + 4 * j) * 4u : kDrop;
+      const uint32_t o = (uint32_t)(base_n + q * 64 + lane);
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o, o, o, o}, orsrc, off, 0u, 0);
+    }
+  }
+  for (int j = 0; j < m1; ++j) {
+#pragma unroll
+    for (int q = 0; q < kC; ++q) {
+      const int len = re[q] - ra[q];
+      const int k = ra[q] + (len & ~3) + j;
+      const uint32_t off = len <= kWide && k < re[q] ? (uint32_t)k * 4u : kDrop;
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(base_n + q * 64 + lane), orsrc, off, 0u, 0);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(wide)) {
+#pragma unroll
+    for (int q = 0; q < kC; ++q) {
+      uint64_t m = __builtin_amdgcn_ballot_w64(re[q] - ra[q] > kWide);
+      while (m) {
+        const int l = __builtin_ctzll(m);
+        m &= m - 1;
+        const int a = __builtin_amdgcn_readlane(ra[q], l);
+        const int e = __builtin_amdgcn_readlane(re[q], l);
+        const uint32_t own = (uint32_t)(base_n + q * 64 + l);
+        for (int k = a; k < e; k += 64) {
+          const int kk = k + lane;
+          __builtin_amdgcn_raw_buffer_store_b32(own, orsrc, kk < e ? (uint32_t)kk * 4u : kDrop, 0u, 0);
+        }
+      }
+    }
+  }
+  // the block's candidate into the sharded winner keys (resample_phase, MODE 0)
+  if (winkey && lane == 0 && bv >= 0)
+    __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, win_key(bv, bi), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave per 256-particle block, four blocks per workgroup (resample_owners_wave).  The loads that do not depend
+// on the control record go out first (both weight slots: the kept one is known only from ctrl); a lane past N
+// loads particle N - 1 (no branch in front of the loads) and is masked afterwards.
+#ifndef PFMPE_RESAMPLE_OWNERS_MIN_WAVES
+#define PFMPE_RESAMPLE_OWNERS_MIN_WAVES 6
+#endif
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_OWNERS_MIN_WAVES))) void
+k_resample_owners(const FrameArgsT<T> fa, const Ctrl* __restrict__ ctrl, const SP* __restrict__ prior,
+                  const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
+                  const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan,
+                  uint32_t* __restrict__ counts, double* __restrict__ mlpose, unsigned long long* __restrict__ winkey) {
+  __shared__ OwnersLds<T> sh;
+  const int wv = wave_id_u();
+  const int blk = (int)blockIdx.x * kWaves + wv;
+  if (blk >= fa.nblk) return;
+  const int lane = lane_id();
+  T wa[4], wb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n = min(blk * kBlock + q * 64 + lane, fa.N - 1);
+    wa[q] = w0[n];
+    wb[q] = w1[n];
+  }
+  const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
+  const GroupScan gs = gscan[blk / fa.gsz];
+  const Ctrl c = *ctrl;
+  if (!c.done || !c.accepted) return;  // unfinished batch or the re-init branch: k_resample_final writes the record
+  const BlockScan bs = c.kept_slot ? bsb : bsa;
+  resample_owners_wave<T, RNG, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), blk, c, prior, w0, w1,
+                                   bs, gs, counts, mlpose, winkey, sh, wv, wa, wb);
 }
 
 // ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first

@@ -378,8 +378,16 @@ inline int ensure_prop(pfmpe_ctx* c) {
     const size_t bytes = (size_t)kPlanes * c->ld * c->es;
     for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc(&c->d_prop[i], bytes));
   }
-  if (c->defer && !c->d_owner[0])
-    for (int i = 0; i < 2; ++i) HIPCHK(c, hipMalloc((void**)&c->d_owner[i], (size_t)c->ld * sizeof(uint32_t)));
+  if (c->defer && !c->d_owner[0]) {  // both or neither: deferral is gated on both pointers
+    const size_t bytes = (size_t)c->ld * sizeof(uint32_t);
+    hipError_t e = hipMalloc((void**)&c->d_owner[0], bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&c->d_owner[1], bytes);
+    if (e != hipSuccess) {
+      if (c->d_owner[0]) (void)hipFree(c->d_owner[0]);
+      c->d_owner[0] = c->d_owner[1] = nullptr;
+      return fail(c, PFMPE_E_HIP, std::string("owner buffers: ") + hipGetErrorString(e));
+    }
+  }
   return PFMPE_OK;
 }
 // the owner indices of the current prior (null: stored in particle order)
@@ -520,11 +528,18 @@ struct Seq {
     // deferred resampling: the new prior's owner indices go to the owner buffer the current prior does not use
     FrameArgsT<T> far = fa;
     c->frame_owner_out = -1;
-    if (kept && c->defer && c->d_owner[0] && !(c->diag & kDiagNoDefer)) {
+    if (kept && c->defer && c->d_owner[0] && c->d_owner[1] && !(c->diag & kDiagNoDefer)) {
       c->frame_owner_out = c->prior_owner == 0 ? 1 : 0;
       far.owner_out = c->d_owner[c->frame_owner_out];
     }
     RET(launch_ext(c, PFMPE_K_RESAMPLE, [&] {
+      // a deferred frame: one wave per 256-particle block (k_resample_owners), same outputs
+      if (far.owner_out && !(c->diag & kDiagBlockResample)) {
+        klaunch(c, k_resample_owners<T, RNG, SP>, dim3((unsigned)((fa.nblk + kWaves - 1) / kWaves)), dim3(kBlock), 0,
+                far, (const Ctrl*)c->d_ctrl, prior, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0],
+                c->d_bscan[1], c->d_gscan, c->record_counts ? c->d_counts : nullptr, c->d_mlpose, c->d_winkey);
+        return;
+      }
       // the kept-set variant compiles the regeneration path out (its registers spilled in the generic form)
       auto k = kept ? k_resample<T, RNG, MAXM, SP, true> : k_resample<T, RNG, MAXM, SP, false>;
       klaunch(c, k, dim3(fa.nblk), dim3(kBlock), 0, far, c->d_ctrl, table,
@@ -764,7 +779,7 @@ struct Seq {
         // stream's prior at take_step, as in finish()) for every state type; without deferral it pays in batches only
         // for fp16 state (round-3 A/B, DESIGN.md §4.2: 8 x C5 batches 5-8 % faster regenerating).  No choice here
         // changes a result.
-        const bool defer = c->defer && c->d_owner[0] && !(c->diag & kDiagNoDefer);
+        const bool defer = c->defer && c->d_owner[0] && c->d_owner[1] && !(c->diag & kDiagNoDefer);
         const bool kept = c->keep_prop && c->d_prop[0] && (defer || std::is_same<SP, __half>::value);
         x.prop0 = kept ? (SP*)c->d_prop[0] : nullptr;
         x.prop1 = kept ? (SP*)c->d_prop[1] : nullptr;

@@ -90,7 +90,7 @@ void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart, c->d_winkey,
                  c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
-                 c->d_stamps};
+                 c->d_stamps, c->d_owner[0], c->d_owner[1]};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -150,7 +150,8 @@ void take_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   c->last_kept_slot = o.kept_slot;
   c->last_kept_iter = o.kept_iter;
   if (o.resampled) {  // newPoseEstimation = resampled set (PE:681, 727), anchored at this frame's current pose
-    if (c->frame_owner_out >= 0 && o.kept_slot >= 0 && o.kept_slot < 2 && c->d_prop[o.kept_slot]) {
+    if (c->frame_owner_out >= 0 && c->d_owner[c->frame_owner_out] && o.kept_slot >= 0 && o.kept_slot < 2 &&
+        c->d_prop[o.kept_slot]) {
       // deferred resampling: the kept buffer is the new prior's storage (read through the owner indices k_resample
       // wrote); the unused post buffer becomes that weight slot's kept buffer for the next frame
       std::swap(c->d_prop[o.kept_slot], c->d_state[1 - c->prior_idx]);
@@ -312,10 +313,13 @@ int pfmpe_set_params(pfmpe_ctx* c, const pfmpe_params* p) {
       (p->rng_mode != PFMPE_RNG_REFERENCE && p->rng_mode != PFMPE_RNG_PHILOX))
     return fail(c, PFMPE_E_ARG, "set_params: invalid parameter");
   const bool retable = c->d_bank && p->tol_pf != c->bank_tol_pf;
+  const pfmpe_params prev = c->params;
   c->params = *p;
   if (retable) {  // the staged bank's grids were built for another tol_PF
-    RET(set_device(c));
-    return build_bank(c);
+    int r = set_device(c);
+    if (r == PFMPE_OK) r = build_bank(c);  // builds the new bank aside; the old one stays until it succeeds
+    if (r != PFMPE_OK) c->params = prev;   // all or nothing: the previous parameters and bank stay in force
+    return r;
   }
   return PFMPE_OK;
 }
@@ -422,27 +426,34 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
 // frame carries a grid whose window is tol_PF's: set_params rebuilds the bank when tol_PF changes, so a bank
 // staged before set_params (or a later change) never leaves the frames on the slower x-bucket path
 // (ADVICE r03).
+// The new bank is built beside the old one and swapped in only once it is on the device, so a failure (an
+// allocation or copy error) leaves the previous bank, its tables and its tol_PF in force.
 static int build_bank(pfmpe_ctx* c) {
   const int nframes = (int)c->bank_offsets.size() - 1;
-  if (c->d_bank) {
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipFree(c->d_bank));
-    c->d_bank = nullptr;
-  }
-  c->bank_off.assign(nframes + 1, 0);
-  c->bank_B.assign(nframes, 0);
-  c->bank_grid.assign(nframes, GridHdr{});
+  std::vector<size_t> off(nframes + 1, 0);
+  std::vector<int32_t> nb(nframes, 0);
+  std::vector<GridHdr> grid(nframes, GridHdr{});
   std::vector<unsigned char> host, one(table_max_bytes(c));
   for (int f = 0; f < nframes; ++f) {
-    c->bank_B[f] = c->bank_offsets[f + 1] - c->bank_offsets[f];
-    const size_t n = build_table(c, c->bank_blobs.data() + 2 * (size_t)c->bank_offsets[f], c->bank_B[f], one.data());
+    nb[f] = c->bank_offsets[f + 1] - c->bank_offsets[f];
+    const size_t n = build_table(c, c->bank_blobs.data() + 2 * (size_t)c->bank_offsets[f], nb[f], one.data());
     host.insert(host.end(), one.begin(), one.begin() + n);
-    c->bank_off[f + 1] = c->bank_off[f] + n;
-    c->bank_grid[f] = *(const GridHdr*)(one.data() + grid_off(c, c->bank_B[f]));
+    off[f + 1] = off[f] + n;
+    grid[f] = *(const GridHdr*)(one.data() + grid_off(c, nb[f]));
   }
-  HIPCHK(c, hipMalloc((void**)&c->d_bank, host.size()));
-  HIPCHK(c, hipMemcpyAsync(c->d_bank, host.data(), host.size(), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // `host` goes out of scope; the frames read the bank in this stream
+  unsigned char* d = nullptr;
+  HIPCHK(c, hipMalloc((void**)&d, host.size()));
+  hipError_t e = hipMemcpyAsync(d, host.data(), host.size(), hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);  // `host` goes out of scope; frames read in this stream
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return fail(c, PFMPE_E_HIP, std::string("build_bank: ") + hipGetErrorString(e));
+  }
+  if (c->d_bank) (void)hipFree(c->d_bank);  // the stream is idle (synchronised above)
+  c->d_bank = d;
+  c->bank_off.swap(off);
+  c->bank_B.swap(nb);
+  c->bank_grid.swap(grid);
   c->bank_tol_pf = c->params.tol_pf;
   return PFMPE_OK;
 }

@@ -17,7 +17,7 @@ def short(name: str) -> str:
     for k in ("k_stage_multi", "k_propagate_weigh_multi", "k_resample_final_multi", "k_resample_multi",
               "k_weigh_pk_multi", "k_group_top_multi", "k_group_multi", "k_top_wide_multi", "k_top_multi",
               "k_weigh_pk", "k_weigh_stream", "k_group_top", "k_group", "k_top_wide", "k_top", "k_propagate_weigh",
-              "k_resample_final", "k_resample", "k_frame2", "k_frame", "k_regen", "k_import", "k_export",
+              "k_resample_final", "k_resample_owners", "k_resample", "k_frame2", "k_frame", "k_regen", "k_import", "k_export",
               "k_weights_export"):
         if k in name:
             return k

@@ -1,0 +1,131 @@
+"""k_resample_owners (one wave per 256-particle block; csrc/pf_kernels.hpp) against k_resample.
+
+A deferred two-launch frame (the kept propagated set, owner indices instead of a materialised prior: every C3 / C4 /
+C5 frame) resamples with k_resample_owners; PFMPE_DIAG 32768 (DIAG_BLOCK_RESAMPLE) runs the block-per-256
+k_resample it replaced.  Both must give the same bits for everything observable, frame after frame: the records
+(winner, most-likely pose, counts of iterations, ...), the weights, both read-backs (the resampled set goes through
+the owner indices) and the resample counts.  Cases:
+  * fp16 / fp32 / fp64 state, both RNG streams, N with a partial last block and a partial last chunk;
+  * a steady frame, an 80-iteration frame (the kept slot moves), it_since_init = 1;
+  * negative weights (self-occlusion penalties): the fp64 scans and running-max scans instead of the shortcuts;
+  * N = 10M fp16 (C4): N >= 2^23, where the winner key's fast path is decided from the counts;
+  * tiny N (one block, one partial chunk).
+"""
+import numpy as np
+import pytest
+
+import pf_monocular_pose_estimator_amd as pf
+from pf_monocular_pose_estimator_amd import synthetic as syn
+from test_gpu_parity import make_engine, _collapsed_scenario
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames(st, occlude_second=True):
+    out = []
+    for f, fr in enumerate(st.frames):
+        blobs, kw = fr.blobs, {}
+        if f == 1 and occlude_second:  # LED 0's blob hidden: the exit rule never fires, 80 iterations
+            uv0 = syn.project(st.K, fr.truth, st.markers)[0]
+            blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
+        if f == 2:
+            kw = {"it_since_init": 1}
+        out.append((fr.current_pose, fr.predicted_pose, fr.prediction, blobs, fr.dt, kw))
+    return out
+
+
+def _run(N, markers, K, state, rng, prior, frames, diag, read=("w", "p0", "p1", "counts"), params=None):
+    eng = make_engine(N, markers, K, state, rng, fused=0, params=params)
+    eng.set_option(pf.OPT_DIAG, diag)
+    eng.set_prior(prior)
+    snaps = []
+    try:
+        for f, (cur, pred, predm, blobs, dt, kw) in enumerate(frames):
+            out = eng.step(eng.make_frame(cur, pred, predm, blobs=blobs, dt=dt, seed=808 + f, frame_idx=f,
+                                          **kw)).as_dict()
+            assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+            snap = {"out": out}
+            if "w" in read:
+                snap["w"] = eng.get_weights()
+            if "p0" in read:
+                snap["p0"] = eng.get_particles(0)
+            if out["resampled"]:
+                if "p1" in read:
+                    snap["p1"] = eng.get_particles(1)
+                if "counts" in read:
+                    snap["counts"] = eng.get_counts()
+            snaps.append(snap)
+    finally:
+        eng.close()
+    return snaps
+
+
+def _assert_same(a_runs, b_runs):
+    assert len(a_runs) == len(b_runs)
+    for f, (a, b) in enumerate(zip(a_runs, b_runs)):
+        for k, v in a["out"].items():
+            assert np.array_equal(np.asarray(v), np.asarray(b["out"][k])), (f, k, v, b["out"][k])
+        assert a.keys() == b.keys(), f
+        for k in a:
+            if k == "out":
+                continue
+            x, y = np.asarray(a[k]), np.asarray(b[k])
+            assert np.array_equal(x, y), (f, k, np.flatnonzero(
+                np.any(x.reshape(len(x), -1) != y.reshape(len(y), -1), axis=1))[:10])
+
+
+CASES = [  # (state, rng, N)
+    (pf.STATE_F16, pf.RNG_PHILOX, 1_200_017),
+    (pf.STATE_F32, pf.RNG_PHILOX, 1_200_017),
+    (pf.STATE_F32, pf.RNG_PHILOX, 300_000),
+    (pf.STATE_F64, pf.RNG_REFERENCE, 4_099),
+    (pf.STATE_F64, pf.RNG_PHILOX, 100_003),
+    (pf.STATE_F32, pf.RNG_REFERENCE, 257),
+    (pf.STATE_F32, pf.RNG_PHILOX, 3),
+]
+
+
+@pytest.mark.parametrize("state,rng,N", CASES)
+def test_owners_equal_block_resample(state, rng, N):
+    st = syn.make_stream(syn.StreamConfig("t", M=5, B=50, N=N), 4)
+    frames = _frames(st)
+    prior = st.prior(fast=True)
+    a = _run(N, st.markers, st.K, state, rng, prior, frames, 0)
+    b = _run(N, st.markers, st.K, state, rng, prior, frames, pf.DIAG_BLOCK_RESAMPLE)
+    if N > 1000:
+        assert a[1]["out"]["iters"] == 80
+    assert any(s["out"]["resampled"] for s in a)
+    _assert_same(a, b)
+
+
+@pytest.mark.parametrize("state", [pf.STATE_F32, pf.STATE_F64])
+def test_owners_negative_weights(state):
+    """_collapsed_scenario's set (positive weights above the accept cap and negative ones from the self-occlusion
+    penalty) repeated over 5,000 particles: waves with and without negative weights side by side."""
+    K, markers, prior64, blobs, truth = _collapsed_scenario()
+    reps = 5000 // prior64.shape[0] + 1
+    prior = np.tile(prior64, (reps, 1))[:5000]
+    N = prior.shape[0]
+    prm = pf.default_params()
+    prm.ang_min = prm.ang_max = prm.trans_min = prm.trans_max = 0.0
+    ident = np.eye(4)[:3].reshape(12)
+    frames = [(truth, truth, ident, blobs, 0.02, {"it_since_init": 1})] * 2
+    rng = pf.RNG_PHILOX
+    a = _run(N, markers, K, state, rng, prior, frames, 0, params=prm)
+    b = _run(N, markers, K, state, rng, prior, frames, pf.DIAG_BLOCK_RESAMPLE, params=prm)
+    assert (a[0]["w"] < 0).any() and (a[0]["w"] > 15).any()
+    assert a[0]["out"]["accepted"] == 1
+    _assert_same(a, b)
+
+
+def test_owners_c4_size():
+    """C4: 10M fp16 particles (N >= 2^23), a steady frame and an 80-iteration one."""
+    cfg = syn.CONFIGS["C4"]
+    st = syn.make_stream(cfg, 2)
+    frames = _frames(st)
+    prior = st.prior(fast=True)
+    read = ("p1", "counts")
+    a = _run(cfg.N, st.markers, st.K, pf.STATE_F16, pf.RNG_PHILOX, prior, frames, 0, read=read)
+    b = _run(cfg.N, st.markers, st.K, pf.STATE_F16, pf.RNG_PHILOX, prior, frames, pf.DIAG_BLOCK_RESAMPLE, read=read)
+    assert a[1]["out"]["iters"] == 80
+    _assert_same(a, b)
