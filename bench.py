@@ -140,6 +140,40 @@ def pmc_traffic(path: str, kernel: str):
         return None
 
 
+# The issue roofline (SURVEY.md §8d "report both fractions"): the kernels of this path have no MFMA work and at the
+# sizes that fit the MALL they are bound by instruction issue, not bytes.  From the committed PMC pass of the same
+# workload (scripts/pmc_lines.sh): VALU issue = SQ_INSTS_VALU (wave instructions) x the measured cost of one wave
+# instruction on its SIMD at >= 4 waves per SIMD, ~4 cycles for this mix (fp64, packed fp32, v_mad_u64_u32, DPP;
+# profiles/r04/isa_rates.txt), over 1,024 SIMDs at 2.4 GHz; SALU issue = SQ_INSTS_SALU over the
+# CU's one scalar unit (256 CUs, one instruction per cycle).  frac = issue time / the kernel's measured time.
+CLOCK_HZ = 2.4e9
+SIMDS, CUS = 1024, 256
+VALU_CYCLES = 4.0
+
+
+def issue_roof(path: str, kernel: str, avg_us: float):
+    if not path or not os.path.exists(path) or not avg_us:
+        return None
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    alias = {"k_frame": "k_frame2", "k_resample": "k_resample_owners"}
+    row = rows.get(kernel) or rows.get(alias.get(kernel, ""), None)
+    if not row or "SQ_INSTS_VALU" not in row or "SQ_INSTS_SALU" not in row:
+        return None
+    t = avg_us * 1e-6
+    valu_s = row["SQ_INSTS_VALU"] * VALU_CYCLES / (SIMDS * CLOCK_HZ)
+    salu_s = row["SQ_INSTS_SALU"] / (CUS * CLOCK_HZ)
+    waves = row.get("SQ_WAVES") or 0
+    return {"bound": "issue", "kernel": kernel, "valu_frac": round(valu_s / t, 4), "salu_frac": round(salu_s / t, 4),
+            "issue_frac": round(max(valu_s, salu_s) / t, 4),
+            "valu_per_wave": round(row["SQ_INSTS_VALU"] / waves, 1) if waves else None,
+            "salu_per_wave": round(row["SQ_INSTS_SALU"] / waves, 1) if waves else None,
+            "valu_cycles": VALU_CYCLES, "clock_ghz": CLOCK_HZ / 1e9, "pmc_source": os.path.relpath(path, ROOT)}
+
+
 def combine_ranks(dist, elapsed: float, updates: float):
     """Whole-job figures: the slowest rank's time (max) and all ranks' particle-updates (sum), over gloo.
     No data-path collective exists: streams are independent, only these two scalars cross ranks."""
@@ -376,6 +410,10 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
             pt["weigh_pass"] = wname
             pt["per_kernel_avg_us"] = {(wname if k == "k_propagate_weigh" else k): round(v[1] * 1e3 / v[0], 3)
                                        for k, v in stats.items() if v[0] > 0}
+            if pt["per_kernel_avg_us"]:
+                dom = max(pt["per_kernel_avg_us"], key=pt["per_kernel_avg_us"].get)
+                pmc = os.path.join(ROOT, "profiles", f"pmc_{cfg.name.lower()}_n{cfg.N}.json")
+                pt["issue"] = issue_roof(pmc, dom, pt["per_kernel_avg_us"][dom])
         return pt
     finally:
         eng.close()
@@ -563,7 +601,8 @@ def main():
                     "frame_level": {"bytes_per_update": upd_bytes, "achieved": round(frame_gbps, 2),
                                     "frac": round(frame_gbps / HBM_PEAK_GBPS, 4),
                                     "what": "updates/s per GPU x (3S+8) B (SURVEY.md §8d), whole frame incl. "
-                                            "launch gaps and the host round trip"}}
+                                            "launch gaps and the host round trip"},
+                    "issue": issue_roof(pmc, dom, avg_s * 1e6)}
         cpu = None
         if world == 1 and args.cpu_frames > 0:
             cpu = cpu_baseline(cfg, args.cpu_frames, args.c1_frames)

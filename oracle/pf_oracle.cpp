@@ -572,6 +572,76 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
 // U_k from the stream position the PF block leaves it at (reference mode: after 12*(N-2)*iters engine
 // outputs; Philox: resample counters), first-i cumulative search.  Used to check the GPU resampler on
 // the GPU's own fp32 weights.  Returns 0 if resampled, 1 if the sum is zero.
+// Particles idx[s] of PF iteration `iter` alone (Philox stream only), each from its prior pose prior[s] (12
+// doubles): the propagated pose (PE:543-588, exactly orc_pf_step's motion model with the same draw ranges) and the
+// literal likelihood (PE:2385-2445).  Philox draws depend only on (particle, iteration, frame, seed), so a sample of
+// a large frame is checked without running the whole frame (tests/test_gpu_packed_oracle.py: the production
+// two-launch packed pass at C4 / C5 sizes against this restatement).  Returns -1 for the reference stream (its
+// draws are addressed through N), 0 otherwise.
+int orc_pf_sample(int n_samples, const int* idx, int M, const double* markers, const double* K,
+                  const uint8_t* downgrade, const orc_params* prm, const orc_frame_in* in, int iter,
+                  const double* prior /*n_samples x 12*/, double* prop_out /*n_samples x 12*/,
+                  double* w_out /*n_samples*/) {
+  if (!prm || !in || prm->rng_mode != RNG_PHILOX || n_samples < 0 || M < 1) return -1;
+  const Mat4 current_pose = from12(in->current_pose);
+  const Mat4 predicted_pose = from12(in->predicted_pose);
+  const Mat4 predictionMatrix = from12(in->prediction);
+  const Mat4 camMoveInv = from12(in->cam_move_inv);
+  double facTrans, facRot;  // PE:488-505 (all three translation factors from predictionMatrix(0,3))
+  if (in->it_since_init == 1) {
+    facTrans = facRot = 1;
+  } else {
+    facTrans = std::min(std::max(0.2, std::abs(predictionMatrix(0, 3)) / in->dt), 1.0) / 4;
+    facRot = 0.2;
+  }
+  std::uniform_real_distribution<double> randTrans(prm->trans_min * facTrans, prm->trans_max * facTrans);
+  std::uniform_real_distribution<double> randAngle(prm->ang_min * facRot, prm->ang_max * facRot);
+  const double lo[6] = {randAngle.a(), randAngle.a(), randAngle.a(), randTrans.a(), randTrans.a(), randTrans.a()};
+  const double hi[6] = {randAngle.b(), randAngle.b(), randAngle.b(), randTrans.b(), randTrans.b(), randTrans.b()};
+  const uint32_t key[2] = {(uint32_t)in->seed, (uint32_t)(in->seed >> 32)};
+  const uint32_t flo = (uint32_t)in->frame_idx, fhi = (uint32_t)(in->frame_idx >> 32);
+  const double g = 1 + prm->growth * std::floor(iter / 10);
+  std::vector<double> proj(2 * (size_t)M);
+  for (int s = 0; s < n_samples; ++s) {
+    const int n = idx[s];
+    Mat4 P;
+    if (n == 0) {
+      P = current_pose;
+    } else if (n == 1) {
+      P = predicted_pose;
+    } else {
+      const Mat4 prior_n = from12(prior + 12 * (size_t)s);
+      Mat4 temp;
+      if (in->it_since_init > 1 && (iter % 10) != 0)
+        temp = mul(mul(camMoveInv, prior_n), predictionMatrix);
+      else if (in->it_since_init > 1)
+        temp = mul(camMoveInv, prior_n);
+      else
+        temp = prior_n;
+      uint32_t ca[4] = {(uint32_t)n, (uint32_t)iter | (0u << 24), flo, fhi}, o[4];
+      philox4x32_10(ca, key, o);
+      const uint32_t v[6] = {o[0] >> 11, o[1] >> 11, o[2] >> 11, o[3] >> 11,
+                             ((o[0] & 0x7FFu) << 10) | (o[1] & 0x3FFu), ((o[2] & 0x7FFu) << 10) | (o[3] & 0x3FFu)};
+      double dr[6];
+      for (int q = 0; q < 6; ++q) dr[q] = u21(v[q]) * (hi[q] - lo[q]) + lo[q];
+      const double a = dr[0] * g, b = dr[1] * g, c = dr[2] * g;
+      Mat4 rotX = identity4(), rotY = identity4(), rotZ = identity4();
+      rotX(1, 1) = std::cos(a); rotX(1, 2) = -std::sin(a); rotX(2, 1) = std::sin(a); rotX(2, 2) = std::cos(a);
+      rotY(0, 0) = std::cos(b); rotY(0, 2) = std::sin(b); rotY(2, 0) = -std::sin(b); rotY(2, 2) = std::cos(b);
+      rotZ(0, 0) = std::cos(c); rotZ(0, 1) = -std::sin(c); rotZ(1, 0) = std::sin(c); rotZ(1, 1) = std::cos(c);
+      P = mul(mul(mul(temp, rotZ), rotY), rotX);
+      P(0, 3) = temp(0, 3) + dr[3] * g;
+      P(1, 3) = temp(1, 3) + dr[4] * g;
+      P(2, 3) = temp(2, 3) + dr[5] * g;
+    }
+    to12(P, prop_out + 12 * (size_t)s);
+    for (int j = 0; j < M; ++j) project2d(K, P, markers + 3 * j, &proj[2 * j]);
+    std::vector<unsigned> pairs;
+    w_out[s] = likelihood_literal(M, in->B, proj.data(), in->blobs, prm->tol, prm->tol_pf, downgrade, pairs);
+  }
+  return 0;
+}
+
 int orc_stratified_resample(int N, const double* raw_weights, int rng_mode, uint64_t seed, uint64_t frame_idx,
                             int iters, unsigned* counts_out, int* idx_out) {
   std::vector<double> w(raw_weights, raw_weights + N);

@@ -114,6 +114,9 @@ def load() -> C.CDLL:
     lib.orc_pf_step.argtypes = [C.c_int, C.c_int, dp, dp, u8p, C.POINTER(OrcParams), C.POINTER(OrcFrameIn), dp,
                                 C.POINTER(OrcFrameOut), dp, dp, dp, C.POINTER(C.c_int), up]
     lib.orc_stratified_resample.restype = C.c_int
+    lib.orc_pf_sample.argtypes = [C.c_int, C.POINTER(C.c_int), C.c_int, dp, dp, u8p, C.POINTER(OrcParams),
+                                  C.POINTER(OrcFrameIn), C.c_int, dp, dp, dp]
+    lib.orc_pf_sample.restype = C.c_int
     lib.orc_stratified_resample.argtypes = [C.c_int, dp, C.c_int, C.c_uint64, C.c_uint64, C.c_int, up,
                                             C.POINTER(C.c_int)]
     lib.orc_exp_map.restype = None
@@ -253,6 +256,40 @@ def pf_step(markers, K, params: OrcParams, prior, current_pose, predicted_pose, 
     if rc != 0:
         raise RuntimeError(f"orc_pf_step failed: {rc}")
     return out.as_dict(), arrays
+
+
+def pf_sample(markers, K, params: OrcParams, idx, prior_rows, current_pose, predicted_pose, prediction, blobs, iter_,
+              it_since_init=2, dt=0.02, seed=1, frame_idx=0, cam_move_inv=None, downgrade=None):
+    """Particles idx of PF iteration iter_ alone (Philox stream), each from its prior pose prior_rows[s]:
+    (propagated poses, literal weights) of orc_pf_sample."""
+    lib = load()
+    m = _d(markers).reshape(-1, 3)
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    pr = _d(prior_rows).reshape(-1, 12)
+    assert pr.shape[0] == idx.shape[0]
+    b = _d(blobs).reshape(-1, 2)
+    fi = OrcFrameIn()
+    fi.current_pose[:] = list(_d(current_pose).reshape(12))
+    fi.predicted_pose[:] = list(_d(predicted_pose).reshape(12))
+    fi.prediction[:] = list(_d(prediction).reshape(12))
+    fi.cam_move_inv[:] = list(np.eye(4)[:3].reshape(12) if cam_move_inv is None else _d(cam_move_inv).reshape(12))
+    fi.blobs = _p(b)
+    fi.B = b.shape[0]
+    fi.it_since_init = it_since_init
+    fi.dt = dt
+    fi.seed = seed
+    fi.frame_idx = frame_idx
+    dg = None
+    if downgrade is not None:
+        dga = np.ascontiguousarray(downgrade, dtype=np.uint8)
+        dg = dga.ctypes.data_as(C.POINTER(C.c_uint8))
+    prop = np.zeros((idx.shape[0], 12))
+    w = np.zeros(idx.shape[0])
+    rc = lib.orc_pf_sample(int(idx.shape[0]), idx.ctypes.data_as(C.POINTER(C.c_int)), m.shape[0], _p(m),
+                           _p(_d(K).reshape(9)), dg, C.byref(params), C.byref(fi), int(iter_), _p(pr), _p(prop), _p(w))
+    if rc != 0:
+        raise RuntimeError(f"orc_pf_sample failed: {rc}")
+    return prop, w
 
 
 def stratified_resample(weights, rng_mode, seed, frame_idx, iters):

@@ -3668,9 +3668,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? P
                                    d.prop1, sc, rec, sh);
 }
 
-// ---- launch 2 of a deferred two-launch frame: stratified resampling of ONE 256-particle block
-// by ONE wave.  The frame has the kept propagated set and defers the new prior (fa.owner_out), so a block's work is
-// its scan, its target counts, its owner indices and its winner key: nothing that needs the block's other waves.
+// ---- launch 2 of a deferred two-launch frame: stratified resampling by waves that each own
+// whole 256-particle blocks.  The frame has the kept propagated set and defers the new prior (fa.owner_out), so a
+// block's work is its scan, its target counts, its owner indices and its winner key: nothing that needs other waves.
 // Lane l handles the block's particles l, 64 + l, 128 + l, 192 + l ("chunks" c = 0..3, exactly the four waves of
 // resample_phase), so every scan keeps resample_phase's association: the chunk's DPP scan, then the earlier chunks'
 // totals added in chunk order (block_incl_from_wave's `pre`), the running maximum carried from chunk to chunk in
@@ -3680,37 +3680,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(KEPT ? P
 // them yields the same bits as its general form wherever it is taken, so the decision granularity does not change
 // any output.  Outputs are resample_phase's for MODE 0 with owner_out: owner_out, counts, the winner key and the
 // most-likely pose (k_resample_final reads the keys, not the count partials, which are therefore not written).
-// No workgroup barrier: the per-wave scalar work (control record, scan words, key schedule, loop control) is paid
-// once per 256 particles instead of once per 64, and a wave never waits for the other three.
+// No workgroup barrier: the per-wave scalar work (control record, kernel arguments, loop control) is paid once per
+// wave, and a wave never waits for another.
+//
+// (Tried: a wave owning 2-4 consecutive blocks, reusing the previous block's last target count as F(rin) when rin is
+// bit-identical to its last R: 10 % fewer VALU and 17 % fewer SALU per particle at C4, but the carried state pushed
+// the kernel past 100 SGPRs (54 spilled to VGPR lanes, scratch) and it measured 0-2 % slower at C4 and 7-22 %
+// slower at C5 (profiles/r05/owners_bpw_ab.txt).)
 template <typename T>
 struct OwnersLds {
   LdsConst<T> sc;  // the frame constants, staged only by the wave holding the most-likely particle
 };
 template <typename T, int RNG, typename SP>
-__device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk,
-                                                     const Ctrl& c, const SP* __restrict__ prior,
-                                                     const T* __restrict__ w0, const T* __restrict__ w1,
-                                                     const BlockScan& bs, const GroupScan& gs,
-                                                     uint32_t* __restrict__ counts, double* __restrict__ mlpose,
-                                                     unsigned long long* __restrict__ winkey, OwnersLds<T>& sh,
-                                                     int wv, const T (&wa)[4], const T (&wb)[4]) {
+__device__ __forceinline__ void resample_owners_block(const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk,
+                                                      const Ctrl& c, const SP* __restrict__ prior,
+                                                      const T* __restrict__ wk, __amdgpu_buffer_rsrc_t orsrc,
+                                                      const BlockScan* __restrict__ bsk,
+                                                      const GroupScan* __restrict__ gscan, uint32_t* __restrict__ counts,
+                                                      double* __restrict__ mlpose, OwnersLds<T>& sh, double& carry_R,
+                                                      int& carry_hi, unsigned long long& key) {
   constexpr int kC = kBlock / 64;
+  constexpr uint32_t kDrop = 0x80000000u;  // a buffer offset past num_records: the access is dropped / reads 0
   const int N = fa.N;
   const int lane = lane_id();
   const int base_n = blk * kBlock;
   const int iters = c.iters;
   const double S = c.S;
   const int64_t Kt = c.K_total;
-  const int slot = c.kept_slot;
+  // the kept weight slot (wk) of the block's four chunks: one lane offset from the block's (uniform) base, the chunk
+  // as an immediate; the weight buffers hold whole blocks (pfmpe_create), a lane past N is masked below
+  const T* wb = wk + base_n;
+  T w[kC];
+#pragma unroll
+  for (int q = 0; q < kC; ++q) w[q] = wb[lane + 64 * q];
+  const BlockScan bs = bsk[blk];
+  const GroupScan gs = gscan[blk / fa.gsz];
   bool valid[kC];
-  double wd[kC];
   bool out_fx = false, out_neg = false;
 #pragma unroll
   for (int q = 0; q < kC; ++q) {
     valid[q] = base_n + q * 64 + lane < N;
-    wd[q] = valid[q] ? (double)(slot ? wb[q] : wa[q]) : 0.0;
-    out_fx |= valid[q] && !(wd[q] >= 0.0 && wd[q] < 32.0);
-    out_neg |= valid[q] && wd[q] < 0.0;
+    w[q] = valid[q] ? w[q] : (T)0;
+    out_fx |= !(w[q] >= (T)0 && w[q] < (T)32);
+    out_neg |= w[q] < (T)0;
   }
   // resample_phase's per-wave choices, taken for the four chunks at once (same bits either way, see above)
   const bool fx = std::is_same<T, float>::value && fa.M >= 4 && __ballot(out_fx) == 0;
@@ -3724,8 +3736,11 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
     const double cz = recip && zn >= 0.0 && zn <= 2.0 * S ? div_by_S(zn, S, c.invS) : zn / S;
     rin = cz > rin ? cz : rin;
   }
-  // F(rin): every lane takes the straight-line common case together, lane 0 alone the rare paths
-  int prev_hi = lane_value(count_targets_wave<T, RNG>(fa, iters, rin, lane == 0), 0);
+  // F(rin): the previous block's last count when rin is its last R, else every lane takes the straight-line common
+  // case together and lane 0 alone the rare paths
+  int prev_hi = carry_hi;
+  if (__double_as_longlong(rin) != __double_as_longlong(carry_R))
+    prev_hi = lane_value(count_targets_wave<T, RNG>(fa, iters, rin, lane == 0), 0);
   double pre = 0.0;  // the earlier chunks' totals, summed in chunk order
   double pm = rin;   // the running max over rin and the earlier chunks
   int ra[kC], re[kC], rc[kC];
@@ -3733,7 +3748,7 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
   int cmax = -1;  // the lane's largest count
 #pragma unroll
   for (int q = 0; q < kC; ++q) {
-    const double wi = fx ? wave_incl_sum_fx((float)wd[q]) : wave_incl_sum(wd[q]);
+    const double wi = fx ? wave_incl_sum_fx((float)w[q]) : wave_incl_sum((double)w[q]);
     const double incl = pre + wi;
     pre = pre + lane_value(wi, 63);
     const double num = gs.G + (bs.E + incl);
@@ -3755,30 +3770,23 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
     if (lane == 0) lo = prev_hi;
     prev_hi = lane_value(hi, 63);
     const int cntn = valid[q] ? hi - lo : 0;
-    const int n = base_n + q * 64 + lane;
-    if (counts && valid[q]) counts[n] = (uint32_t)cntn;
-    // write range [a, e) (resample_phase: targets past K_total copy the last found particle, PE:681)
-    int a, e;
-    if (!valid[q]) {
-      a = e = N;
-    } else if (Kt == 0) {
+    if (counts) counts[base_n + lane + 64 * q] = (uint32_t)cntn;  // (whole blocks allocated: pfmpe_create)
+    // write range [a, e) (resample_phase: targets past K_total copy the last found particle, PE:681), as selects
+    int a = lo, e = hi == Kt ? N : hi;
+    a = lo >= Kt ? N : a;
+    e = lo >= Kt ? N : e;
+    if (Kt == 0) {  // (wave-uniform) no target found a particle: every slot copies the last one
       a = 0;
-      e = (n == N - 1) ? N : 0;
-    } else if (lo >= Kt) {
-      a = e = N;
-    } else if (hi == Kt) {
-      a = lo;
-      e = N;
-    } else {
-      a = lo;
-      e = hi;
+      e = base_n + q * 64 + lane == N - 1 ? N : 0;
     }
-    ra[q] = a;
-    re[q] = e;
+    ra[q] = valid[q] ? a : N;
+    re[q] = valid[q] ? e : N;
     rc[q] = valid[q] ? cntn : -1;
     kmax = max(kmax, valid[q] ? cntn * 256 + (255 - (q * 64 + lane)) : -1);  // (unused if a count is >= 2^23)
     cmax = max(cmax, rc[q]);
   }
+  carry_R = pm;        // the block's last R (its last particle's, when that one is valid)
+  carry_hi = prev_hi;  // F of it
   // block max count, first index (the winner candidate): one integer key unless some count is >= 2^23 (always below
   // at N < 2^23; at larger N all but degenerate frames)
   int bv, bi;
@@ -3799,6 +3807,10 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
 #pragma unroll
     for (int q = 0; q < kC; ++q) cmb_max(bv, bi, rc[q], rc[q] >= 0 ? base_n + q * 64 + lane : 0x7fffffff);
     wave_argmax(bv, bi);
+  }
+  if (bv >= 0) {  // the wave's key: max over its blocks (win_key orders as (count, lowest index))
+    const unsigned long long kb = win_key(bv, bi);
+    key = kb > key ? kb : key;
   }
 
   // the most likely pose for the frame record (write-through), regenerated by its lane (the kept set holds stored
@@ -3821,22 +3833,22 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
   // Owner indices: particle p of the block owns the slots [ra, re) of its lane and chunk (consecutive, non-empty
   // ranges in particle order).  Each lane writes its own particles' ranges: first 16-B stores of four slots while at
   // least four remain, then single slots; a store past its range goes to an offset the buffer's range check drops
-  // (no exec-mask branches).  In a typical frame every range is a few slots and the lanes' ranges are adjacent, so a
-  // round's stores fall on a few consecutive lines; where the weight concentrates (ranges of tens of slots in a whole
-  // region of the set) the 16-B stores quarter the write transactions.  A range longer than kWide (one particle
-  // taking a large share of the targets) is written by the whole wave, 64 consecutive slots per store, one such
-  // particle after another.
+  // (no exec-mask branches), the round's step in soffset.  In a typical frame every range is a few slots and the
+  // lanes' ranges are adjacent, so a round's stores fall on a few consecutive lines; where the weight concentrates
+  // (ranges of tens of slots over a whole region of the set) the 16-B stores quarter the write transactions.  A range
+  // longer than kWide (one particle taking a large share of the targets) is written by the whole wave, 64
+  // consecutive slots per store, one such particle after another.
   constexpr int kWide = 256;
-  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc((void*)fa.owner_out, (short)0, (int)(N * 4),
-                                                                          0x00020000);
-  constexpr uint32_t kDrop = 0x80000000u;  // past num_records: the store is dropped
+  int nq[kC], nr[kC];
   int m4 = 0, m1 = 0;
   bool wide = false;
 #pragma unroll
   for (int q = 0; q < kC; ++q) {
     const int len = re[q] - ra[q];
-    m4 = max(m4, len <= kWide ? len >> 2 : 0);
-    m1 = max(m1, len <= kWide ? len & 3 : 0);
+    nq[q] = len <= kWide ? len >> 2 : 0;
+    nr[q] = len <= kWide ? len & 3 : 0;
+    m4 = max(m4, nq[q]);
+    m1 = max(m1, nr[q]);
     wide |= len > kWide;
   }
   m4 = max(m4, __builtin_amdgcn_mov_dpp(m4, kDppQuadXor1, 0xf, 0xf, true));
@@ -3849,23 +3861,26 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
   // the largest remainder (<= 3) by ballots
   m1 = __builtin_amdgcn_ballot_w64(m1 >= 3) ? 3 : __builtin_amdgcn_ballot_w64(m1 >= 2) ? 2
                                                 : __builtin_amdgcn_ballot_w64(m1 >= 1) ? 1 : 0;
-  for (int j = 0; j < m4; ++j) {
+  if (m4 > 0) {
+    u32x4_t o4[kC];
 #pragma unroll
     for (int q = 0; q < kC; ++q) {
-      const int len = re[q] - ra[q];
-      const uint32_t off = len <= kWide && 4 * j + 4 <= len ? (uint32_t)(ra[q] + 4 * j) * 4u : kDrop;
       const uint32_t o = (uint32_t)(base_n + q * 64 + lane);
-      __builtin_amdgcn_raw_buffer_store_b128(u32x4_t{o, o, o, o}, orsrc, off, 0u, 0);
+      o4[q] = u32x4_t{o, o, o, o};
+    }
+    for (int j = 0; j < m4; ++j) {
+#pragma unroll
+      for (int q = 0; q < kC; ++q)
+        __builtin_amdgcn_raw_buffer_store_b128(o4[q], orsrc, j < nq[q] ? (uint32_t)ra[q] * 4u : kDrop,
+                                               (uint32_t)(16 * j), 0);
     }
   }
   for (int j = 0; j < m1; ++j) {
 #pragma unroll
-    for (int q = 0; q < kC; ++q) {
-      const int len = re[q] - ra[q];
-      const int k = ra[q] + (len & ~3) + j;
-      const uint32_t off = len <= kWide && k < re[q] ? (uint32_t)k * 4u : kDrop;
-      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(base_n + q * 64 + lane), orsrc, off, 0u, 0);
-    }
+    for (int q = 0; q < kC; ++q)
+      __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(base_n + q * 64 + lane), orsrc,
+                                            j < nr[q] ? (uint32_t)(ra[q] + 4 * nq[q]) * 4u : kDrop, (uint32_t)(4 * j),
+                                            0);
   }
   if (__builtin_amdgcn_ballot_w64(wide)) {
 #pragma unroll
@@ -3884,15 +3899,9 @@ __device__ __forceinline__ void resample_owners_wave(const FrameArgsT<T>& fa, co
       }
     }
   }
-  // the block's candidate into the sharded winner keys (resample_phase, MODE 0)
-  if (winkey && lane == 0 && bv >= 0)
-    __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, win_key(bv, bi), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One wave per 256-particle block, four blocks per workgroup (resample_owners_wave).  The loads that do not depend
-// on the control record go out first (both weight slots: the kept one is known only from ctrl); a lane past N
-// loads particle N - 1 (no branch in front of the loads) and is masked afterwards.
+// One wave per block, four per workgroup.
 #ifndef PFMPE_RESAMPLE_OWNERS_MIN_WAVES
 #define PFMPE_RESAMPLE_OWNERS_MIN_WAVES 6
 #endif
@@ -3903,24 +3912,51 @@ k_resample_owners(const FrameArgsT<T> fa, const Ctrl* __restrict__ ctrl, const S
                   const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan,
                   uint32_t* __restrict__ counts, double* __restrict__ mlpose, unsigned long long* __restrict__ winkey) {
   __shared__ OwnersLds<T> sh;
-  const int wv = wave_id_u();
-  const int blk = (int)blockIdx.x * kWaves + wv;
+  const int blk = (int)blockIdx.x * kWaves + wave_id_u();
   if (blk >= fa.nblk) return;
-  const int lane = lane_id();
-  T wa[4], wb[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int n = min(blk * kBlock + q * 64 + lane, fa.N - 1);
-    wa[q] = w0[n];
-    wb[q] = w1[n];
-  }
-  const BlockScan bsa = bscan0[blk], bsb = bscan1[blk];
-  const GroupScan gs = gscan[blk / fa.gsz];
   const Ctrl c = *ctrl;
   if (!c.done || !c.accepted) return;  // unfinished batch or the re-init branch: k_resample_final writes the record
-  const BlockScan bs = c.kept_slot ? bsb : bsa;
-  resample_owners_wave<T, RNG, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), blk, c, prior, w0, w1,
-                                   bs, gs, counts, mlpose, winkey, sh, wv, wa, wb);
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void*)fa.owner_out, (short)0, fa.N * 4, 0x00020000);
+  double carry_R = __longlong_as_double(0x7ff8dead00000000ll);  // a NaN no R equals bitwise: evaluate F(rin)
+  int carry_hi = 0;
+  unsigned long long key = 0ull;
+  resample_owners_block<T, RNG, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), blk, c, prior,
+                                    c.kept_slot ? w1 : w0, ors, c.kept_slot ? bscan1 : bscan0, gscan, counts, mlpose,
+                                    sh, carry_R, carry_hi, key);
+  // the block's candidate into the sharded winner keys (resample_phase, MODE 0)
+  if (key && lane_id() == 0)
+    __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, key, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The batched form (pfmpe_step_multi, every stream deferred): wave i of the grid takes the batch's block i, its
+// stream from the block map (batch_block's checks, per wave).  Batches keep the count partials k_resample_final_multi
+// reduces (no winner keys): the wave's candidate goes to its block's partial.
+template <typename T, int RNG, typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_OWNERS_MIN_WAVES))) void
+k_resample_owners_multi(const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S,
+                        const uint32_t* __restrict__ status, uint32_t gen, int total) {
+  __shared__ OwnersLds<T> sh;
+  const int gb = (int)blockIdx.x * kWaves + wave_id_u();
+  if (gb >= total) return;
+  const int s = __builtin_amdgcn_readfirstlane((int)bmap[gb]);
+  if (s >= S || __builtin_amdgcn_readfirstlane(status[s]) != gen) return;
+  const StreamDesc<T, SP>& d = descs[s];
+  const int blk = gb - __builtin_amdgcn_readfirstlane(d.first_blk);
+  if (blk < 0 || blk >= __builtin_amdgcn_readfirstlane(d.fa.nblk)) return;
+  const Ctrl c = load_ctrl_uniform(d.ctrl);
+  if (!c.done || !c.accepted) return;
+  const __amdgpu_buffer_rsrc_t ors =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.fa.owner_out, (short)0, d.fa.N * 4, 0x00020000);
+  double carry_R = __longlong_as_double(0x7ff8dead00000000ll);
+  int carry_hi = 0;
+  unsigned long long key = 0ull;
+  resample_owners_block<T, RNG, SP>(d.fa, (const uint32_t*)&d.fa, blk, c, d.prior, c.kept_slot ? d.w1 : d.w0, ors,
+                                    c.kept_slot ? d.bscan1 : d.bscan0, d.gscan, d.counts, d.mlpose, sh, carry_R,
+                                    carry_hi, key);
+  if (lane_id() == 0)  // every block has a valid particle, so a key (count 0 included): win_key decoded
+    d.cpart[blk] = CountPart{(int32_t)(key >> 32), 0x7fffffff - (int32_t)(uint32_t)key};
 }
 
 // ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first
@@ -4407,20 +4443,31 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
 #ifndef PFMPE_FRAME2_MIN_WAVES
 #define PFMPE_FRAME2_MIN_WAVES 1
 #endif
+// The LDS of a k_frame2 block (the one-launch kernel and the resident frame server share the body)
+template <typename T>
+struct Frame2Shared {
+  LdsConst<T> sc;
+  WeighLds wsh;
+  ResampleLds<T> rsh;
+  OutDev rec;
+  Frame2Lds fl;
+};
+// One frame of k_frame2 for this block.  fa_words: the frame arguments as words (the kernarg segment, or the
+// server's ring slot) for the LDS constants.  Returns false when the block gave up at the weighing barrier's
+// bound (an abandoned frame: no record).
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_MIN_WAVES))) void k_frame2(
-    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
-    SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
-    BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart,
-    uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
-    double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ LdsConst<T> sc;
-  __shared__ WeighLds wsh;
-  __shared__ ResampleLds<T> rsh;
-  __shared__ OutDev rec;
-  __shared__ Frame2Lds fl;
-
+__device__ __forceinline__ bool frame2_body(
+    const FrameArgsT<T>& fa, const uint32_t* fa_words, const unsigned char* __restrict__ table,
+    const SP* __restrict__ prior, SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1,
+    BlockPart* __restrict__ part0, BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl,
+    CountPart* __restrict__ cpart, uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
+    double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps,
+    unsigned char* smem, Frame2Shared<T>& S2) {
+  LdsConst<T>& sc = S2.sc;
+  WeighLds& wsh = S2.wsh;
+  ResampleLds<T>& rsh = S2.rsh;
+  OutDev& rec = S2.rec;
+  Frame2Lds& fl = S2.fl;
   if (stamps && threadIdx.x == 0) stamp_min(stamps, 0, rt_now());
   const int n = blockIdx.x * kBlock + threadIdx.x;
   const bool valid = n < fa.N;
@@ -4430,7 +4477,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   copy_table(table, smem, (size_t)fa.tbytes);
   T A[12];
   if (valid && n >= 2) load_prior(fa, prior, n, A);
-  stage_consts(fa, sc);
+  stage_consts_from(fa_words, sc);
   if (threadIdx.x == 0) {
     fl.c = zero_ctrl();  // start of frame: every block keeps an identical copy of the control record
     fl.abort = 0;
@@ -4507,7 +4554,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
         if (lane == 0 && !ok) fl.abort = 1;
       }
       __syncthreads();
-      if (fl.abort) return;
+      if (fl.abort) return false;
     }
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 2, rt_now());
     // every block: the group partials from all block partials, then the top.  Groups are 64 blocks, so
@@ -4588,7 +4635,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   if (!c.accepted) {  // re-init branch (PE:707-719): no resampling, record only
     if (blk == 0 && wv == 0)
       finalize_frame<T, RNG, MAXM, SP>(fa, sc, c, ctrl, prior, -1, cand, mlpose, rec, out, 2 * seq + 1, stamps);
-    return;
+    return true;
   }
   const int kslot = c.kept_slot;
   const bool have_P = c.kept_iter == iter;
@@ -4598,6 +4645,147 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   const GroupScan gs = fl.gs;
   resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
                                       mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq, stamps, flat, blk);
+  return true;
+}
+
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_MIN_WAVES))) void k_frame2(
+    const FrameArgsT<T> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1, BlockPart* __restrict__ part0,
+    BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl, CountPart* __restrict__ cpart,
+    uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
+    double* __restrict__ mlpose, RecOut* __restrict__ out, int32_t seq, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ Frame2Shared<T> S2;
+  (void)frame2_body<T, RNG, MAXM, PRUNE, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), table, prior,
+                                             post, w0, w1, part0, part1, ctrl, cpart, flat, counts, cand, mlpose, out,
+                                             seq, stamps, smem, S2);
+}
+
+// ---- the resident frame server (PFMPE_OPT_RESIDENT): k_frame2's blocks stay resident across
+// frames and take each frame from a host mailbox instead of a launch.  A one-launch frame at C2 is ~25 us of kernel
+// behind ~10 us of host launch and dispatch (hipLaunchKernel's own ~7 us of host time, then the dispatch of 391
+// blocks); the server replaces that with a doorbell: the host writes the frame's message (the kernel arguments of
+// k_frame2, its buffers, an inline blob table for host blobs) into pinned memory and then the doorbell word.
+//  * Block 0's wave 0 polls the doorbell (system-scope loads of host memory), copies the message into ring slot j
+//    of device memory (one slot per frame of this dispatch: the scalar cache holds no line of a slot before its
+//    frame, so the frame's arguments can be read with scalar loads, as kernel arguments are) and publishes j + 1
+//    on a device word (release).
+//  * Every block's wave 0 polls that word (agent scope), the block takes an agent-scope acquire (its L1 lines of
+//    last frame's buffers are dropped, as a new dispatch would), and runs frame2_body on the slot.
+//  * Every wait is bounded: the doorbell by idle_ticks (then the server exits by itself; the host restarts it
+//    before that can matter, pfmpe_ctx.hpp kSrvIdleNs), the slot word by the same bound, the frame's own barriers
+//    by its wait bound.  A frame abandoned at a barrier sets the exit bit, so every block returns; the host then
+//    finds no record and redoes the frame with launches.  An exit message ends the server (the host's stop), and
+//    the server ends by itself after its last ring slot (the host relaunches it then).
+template <typename T, typename SP>
+struct alignas(256) SrvMsg {
+  FrameArgsT<T> fa;
+  const unsigned char* table;  // the frame's blob table in device memory (bank), or null: inline, after the message
+  const SP* prior;
+  SP* post;
+  int32_t seq, exit_;
+  int32_t tinl;  // bytes of the inline table (a multiple of 8; 0: `table`)
+  int32_t pad;
+};
+// host mailbox layout (pinned): the doorbell, the per-frame device durations, the message (+ inline table)
+constexpr int kSrvSlots = 256;                        // frames per server dispatch (ring slots)
+constexpr size_t kSrvDurOff = 256;                    // uint64 dur[kSrvSlots]: s_memrealtime ticks, frame j
+constexpr size_t kSrvMsgOff = kSrvDurOff + 8 * kSrvSlots;
+constexpr uint32_t kSrvExit = 0x80000000u;            // the slot word's exit bit
+
+// 3 waves per SIMD: two resident blocks per CU next to the occupancy margin, as a one-launch k_frame2 needs
+// (pfmpe_ctx.hpp frame_fused); unconstrained, the frame loop's live state took the server past 168 VGPRs
+#ifndef PFMPE_FRAME2_SRV_MIN_WAVES
+#define PFMPE_FRAME2_SRV_MIN_WAVES 3
+#endif
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_SRV_MIN_WAVES))) void k_frame2_srv(
+    const unsigned char* __restrict__ host, unsigned char* __restrict__ ring,
+    const __attribute__((address_space(4))) unsigned char* ring_c, uint32_t slot_bytes, int nslots,
+    uint32_t* __restrict__ dseq, uint32_t idle_ticks, T* __restrict__ w0, T* __restrict__ w1,
+    BlockPart* __restrict__ part0, BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl,
+    CountPart* __restrict__ cpart, uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
+    double* __restrict__ mlpose, RecOut* __restrict__ out, uint64_t* __restrict__ stamps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ Frame2Shared<T> S2;
+  __shared__ int s_exit, s_zero;
+  using Msg = SrvMsg<T, SP>;
+  static_assert(sizeof(Msg) % 256 == 0, "ring slots on whole lines");
+  auto host_ld = [](const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+  // every test below is wave-uniform by construction (the wave index through an SGPR, LDS flags through
+  // readfirstlane): the frame loop's index then stays uniform, and with it the slot address whose words the body
+  // reads as scalars
+  const int lane = lane_id(), wv = wave_id_u();
+  for (int j = 0; j < nslots; ++j) {
+    unsigned char* slot = ring + (size_t)j * slot_bytes;
+    uint64_t t0 = 0;
+    if (blockIdx.x == 0 && wv == 0) {
+      const uint64_t* bell = (const uint64_t*)host;
+      const uint64_t start = rt_now();
+      bool ok = false;
+      for (;;) {  // bounded: idle_ticks
+        if (host_ld(bell) >= (uint64_t)(j + 1)) {
+          ok = true;
+          break;
+        }
+        if (rt_now() - start > (uint64_t)idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      t0 = rt_now();
+      int quit = 1;
+      if (ok) {
+        const uint64_t* src = (const uint64_t*)(host + kSrvMsgOff);
+        uint64_t* dst = (uint64_t*)slot;
+        constexpr int kW = (int)(sizeof(Msg) / 8);
+        for (int i = lane; i < kW; i += 64) dst[i] = host_ld(src + i);
+        const uint64_t ex = host_ld(src + offsetof(Msg, exit_) / 8);  // {exit_, tinl}
+        quit = (int)(uint32_t)ex;
+        const int tw = (int)(uint32_t)(ex >> 32) / 8;
+        for (int i = lane; i < tw; i += 64) dst[kW + i] = host_ld(src + kW + i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot is in L2 before its word
+      }
+      if (lane == 0)
+        __hip_atomic_store(dseq, (uint32_t)(j + 1) | (quit ? kSrvExit : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (wv == 0) {  // every block: the slot's word (bounded as the doorbell, plus a margin)
+      const uint64_t start = rt_now();
+      uint32_t v;
+      for (;;) {
+        v = __hip_atomic_load(dseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & kSrvExit) || (v & ~kSrvExit) >= (uint32_t)(j + 1)) break;
+        if (rt_now() - start > 2ull * idle_ticks) {
+          v = kSrvExit;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0) {
+        s_exit = (v & kSrvExit) ? 1 : 0;
+        s_zero = (int)(v & 0u);  // 0, through LDS: the slot's address depends on the wait (below)
+      }
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(s_exit)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // as a new dispatch: no L1 line of last frame's buffers
+    // The slot's words as CONSTANT memory (scalar loads, SGPR operands, as kernel arguments): correct because the
+    // slot is written once per dispatch (the scalar cache holds none of its lines before this frame) and before
+    // its word is published; the address depends on the LDS word read after the wait, so no load moves above it.
+    typedef __attribute__((address_space(4))) const Msg CMsg;
+    const CMsg* mc = (const CMsg*)(ring_c + (size_t)j * slot_bytes + __builtin_amdgcn_readfirstlane(s_zero));
+    const Msg* m = (const Msg*)mc;
+    const unsigned char* table = m->tinl ? slot + sizeof(Msg) : m->table;
+    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP>(m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post, w0,
+                                                         w1, part0, part1, ctrl, cpart, flat, counts, cand, mlpose, out,
+                                                         m->seq, stamps, smem, S2);
+    if (!__builtin_amdgcn_readfirstlane((int)ok)) {
+      if (threadIdx.x == 0) __hip_atomic_fetch_or(dseq, kSrvExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;  // abandoned at a barrier: every block leaves (the host redoes the frame with launches)
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // the frame's device time: doorbell seen -> block 0 done (record out)
+      __hip_atomic_store((uint64_t*)(host + kSrvDurOff) + j, rt_now() - t0, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path).  anchor: the set's

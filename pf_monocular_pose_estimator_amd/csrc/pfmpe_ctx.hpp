@@ -749,6 +749,7 @@ struct Seq {
       int64_t total = 0;
       size_t lds_w = 0, lds_f = 0;
       bool all_kept = true;  // every stream has its kept propagated set: k_resample_multi<KEPT = true>
+      bool all_owners = true;  // ... and defers its new prior: k_resample_owners_multi
       if (++c0->multi_gen == 0u || c0->multi_gen == ~0u) c0->multi_gen = 1u;  // never 0 / ~0 (status words)
       const uint32_t gen = c0->multi_gen;
       std::vector<Desc> want(na);  // the descriptors as written (the staging check's reference for a report)
@@ -788,6 +789,8 @@ struct Seq {
         if (kept && defer) {
           c->frame_owner_out = c->prior_owner == 0 ? 1 : 0;
           x.fa.owner_out = c->d_owner[c->frame_owner_out];
+        } else {
+          all_owners = false;
         }
         x.cpart = c->d_cpart;
         x.cgroup = c->d_cgroup;
@@ -898,7 +901,10 @@ struct Seq {
       }
       for (int i = 0; i < na; ++i) cs[act[i]]->last_weigh_pass = pk ? PFMPE_WEIGH_PK : PFMPE_WEIGH_BLOCKS;
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
-        if (all_kept)
+        if (all_owners && !(c0->diag & kDiagBlockResample))  // a wave per block (§4.2d)
+          klaunch(c0, k_resample_owners_multi<T, RNG, SP>, dim3((unsigned)((total + kWaves - 1) / kWaves)), dim3(kBlock),
+                  0, dd, db, na, (const uint32_t*)dstat, gen, (int)total);
+        else if (all_kept)
           klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
                   (const uint32_t*)dstat, gen);
         else

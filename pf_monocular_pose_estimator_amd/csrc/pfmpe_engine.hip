@@ -226,7 +226,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   c->max_grp = c->max_blk;  // groups hold ~sqrt(blocks) blocks (build_args): size group buffers per block
   for (int i = 0; i < 2; ++i) {
     ok &= hipMalloc(&c->d_state[i], state_bytes) == hipSuccess;
-    ok &= hipMalloc(&c->d_w[i], (size_t)c->ld * c->ws) == hipSuccess;
+    ok &= hipMalloc(&c->d_w[i], (size_t)c->max_blk * kBlock * c->ws) == hipSuccess;  // whole blocks: k_resample_owners
     // kWaves entries per block: the streaming weighing pass stores wave partials (k_group combines them)
     ok &= hipMalloc((void**)&c->d_part[i], (size_t)c->max_blk * kWaves * sizeof(BlockPart)) == hipSuccess;
     ok &= hipMalloc((void**)&c->d_bscan[i], (size_t)c->max_blk * sizeof(BlockScan)) == hipSuccess;
@@ -331,7 +331,7 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       c->record_counts = value != 0;
       if (c->record_counts && !c->d_counts) {
         RET(set_device(c));
-        HIPCHK(c, hipMalloc((void**)&c->d_counts, (size_t)c->ld * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void**)&c->d_counts, (size_t)c->max_blk * kBlock * sizeof(uint32_t)));  // whole blocks
       }
       return PFMPE_OK;
     case PFMPE_OPT_FUSED:

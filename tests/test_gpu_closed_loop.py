@@ -160,3 +160,24 @@ def test_closed_loop_100k_fp16():
     against the fp64 oracle loop."""
     cfg = syn.StreamConfig("C2f16", M=5, B=50, N=100_000)
     assert_within(run_pair(cfg, 20, pf.STATE_F16, pf.RNG_PHILOX), 0.95, "100k fp16")
+
+
+def _packed_shape(eng, out, ref, arr):
+    """The frame ran the production two-launch shape: k_weigh_pk, then k_resample_owners (deferred)."""
+    assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+    assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_PK
+    assert out["iters"] == ref["iters"] and out["accepted"] == ref["accepted"]
+
+
+def test_closed_loop_c5_fp32_packed():
+    """C5's stream (BASELINE.json configs[4]: 5 LEDs, 50 blobs, 1M particles, fp32) over 10 frames in the production
+    two-launch shape (k_weigh_pk + k_resample_owners, deferred prior) against the fp64 oracle loop (VERDICT r04
+    missing 2: the packed pass had been checked against the oracle only through bit-identity chains)."""
+    assert_within(run_pair(syn.CONFIGS["C5"], 10, pf.STATE_F32, pf.RNG_PHILOX, _packed_shape), 0.95, "C5 fp32 packed")
+
+
+def test_closed_loop_1m_fp16_packed():
+    """fp16-delta state (C4's storage) at 1M particles over 5 frames in the production two-launch shape against the
+    fp64 oracle loop."""
+    cfg = syn.StreamConfig("C4s", M=5, B=50, N=1_000_000)
+    assert_within(run_pair(cfg, 5, pf.STATE_F16, pf.RNG_PHILOX, _packed_shape), 0.95, "1M fp16 packed")

@@ -1,0 +1,111 @@
+"""The production two-launch packed path at full size (C4: 10M fp16, C5: 1M fp32) against the CPU oracle directly.
+
+C4 and C5 frames run k_weigh_pk (two particles per lane, packed fp32; pf_weigh_pk.hpp), which stores each particle's
+propagated pose in the kept set, then k_resample_owners, whose owner indices make the kept set the next prior.  The
+oracle cannot run a 10M-particle frame, but its Philox draws depend only on (particle, iteration, frame, seed), so
+orc_pf_sample (oracle/pf_oracle.cpp, the motion model PE:543-588 and the literal likelihood PE:2385-2445 of
+orc_pf_step) restates any sampled particle from its prior row.  Per frame, for 2,000 sampled slots k of the new prior
+and their owners i (reconstructed from the resample counts: slot k belongs to the particle whose cumulative count
+range holds k, PE:666-682):
+  * the new prior row k (the kept set's stored pose of particle i, read back through the owner indices) equals the
+    oracle's propagation of particle i from its prior row at the kept iteration, within 1e-5 (fp32) or the fp16
+    delta quantum (|pose - anchor| * 2^-10 + 1e-6; the anchor is the frame's current pose);
+  * the engine's weight of particle i equals the oracle's literal likelihood within 2e-3 on >= 99.5 % of the
+    samples (a marker within ~1e-5 px of the tol_PF gate may flip);
+  * the pass that ran is k_weigh_pk and the frame shape is two launches.
+Frames: a steady frame, an 80-iteration frame (one LED hidden: predictionMatrix composition from iteration 1, noise
+growth from iteration 10, the kept iteration not the last) and an it_since_init = 1 frame (fac = 1 draw ranges).
+"""
+import numpy as np
+import pytest
+
+import pf_monocular_pose_estimator_amd as pf
+from pf_monocular_pose_estimator_amd import synthetic as syn
+from oracle import pforacle as orc
+
+pytestmark = pytest.mark.gpu
+
+N_SAMPLES = 2000
+
+
+def _frames(st):
+    """(current pose, predicted pose, prediction, blobs, dt, it_since_init) per frame."""
+    out = []
+    for f, fr in enumerate(st.frames):
+        cur, pred, blobs, it = np.array(fr.current_pose), np.array(fr.predicted_pose), fr.blobs, 2
+        if f == 1:  # LED 0's blob hidden and particles 0 / 1 5 cm off: 80 iterations, a late iteration kept
+            uv0 = syn.project(st.K, fr.truth, st.markers)[0]
+            blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
+            cur[3] += 0.05
+            pred[3] += 0.05
+        if f == 2:
+            it = 1
+        out.append((cur, pred, np.array(fr.prediction), blobs, fr.dt, it))
+    return out
+
+
+def owners_from_counts(counts):
+    """Slot -> owner of the stratified resampling (PE:666-682): counts[i] consecutive slots for particle i in
+    index order; targets past the last found one (rounding) copy the last found particle (PE:681)."""
+    N = counts.shape[0]
+    own = np.repeat(np.arange(N, dtype=np.int64), counts.astype(np.int64))
+    if own.shape[0] < N:
+        own = np.concatenate([own, np.full(N - own.shape[0], own[-1] if own.shape[0] else N - 1)])
+    return own[:N]
+
+
+@pytest.mark.parametrize("name,state", [("C5", pf.STATE_F32), ("C4", pf.STATE_F16)])
+def test_packed_path_against_oracle(name, state):
+    cfg = syn.CONFIGS[name]
+    N = cfg.N
+    st = syn.make_stream(cfg, 3)
+    eng = pf.Engine(device=0, max_particles=N, state_dtype=state)
+    rng = np.random.default_rng(55)
+    prm = pf.default_params()
+    op = orc.make_params(rng_mode=orc.RNG_PHILOX)
+    worst_p, worst_w, flips = 0.0, 0.0, 0
+    try:
+        eng.set_model(st.markers, st.K)
+        eng.set_params(prm)
+        eng.set_option(pf.OPT_FUSED, 0)
+        eng.set_option(pf.OPT_RECORD_COUNTS, 1)
+        eng.set_prior(st.prior(fast=True))
+        for f, (cur, pred, predm, blobs, dt, it) in enumerate(_frames(st)):
+            prior = eng.get_particles(1)  # the prior rows as the engine holds them (fp16: dequantised)
+            seed = 3000 + f
+            out = eng.step(eng.make_frame(cur, pred, predm, blobs=blobs, dt=dt, seed=seed, frame_idx=f,
+                                          it_since_init=it)).as_dict()
+            assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+            assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_PK
+            assert out["accepted"] == 1 and out["resampled"] == 1, (f, out["flag_fail"])
+            if f == 1:
+                assert out["iters"] == 80
+                print(f"{name} frame 1: kept iteration {out['kept_iter']}")
+            w = eng.get_weights()
+            counts = eng.get_counts()
+            assert int(counts.sum()) <= N
+            post = eng.get_particles(1)  # the new prior: the kept set read through the owner indices
+            own = owners_from_counts(counts)
+            slots = np.unique(np.concatenate([rng.choice(N, N_SAMPLES, replace=False), [0, N - 1]]))
+            idx = own[slots]
+            ref_p, ref_w = orc.pf_sample(st.markers, st.K, op, idx, prior[idx], cur, pred, predm, blobs,
+                                         out["kept_iter"], dt=dt, seed=seed, frame_idx=f, it_since_init=it)
+            got = post[slots]
+            if state == pf.STATE_F16:
+                anchor = cur.reshape(1, 12)
+                tol = np.abs(ref_p - anchor) * 2.0 ** -10 + 1e-6
+            else:
+                tol = np.full(ref_p.shape, 1e-5)
+            err = np.abs(got - ref_p)
+            bad = np.argwhere(err > tol)
+            assert bad.shape[0] == 0, (f, bad[:5], err[tuple(bad[0])] if bad.shape[0] else None)
+            worst_p = max(worst_p, float(err.max()))
+            dw = np.abs(w[idx] - ref_w)
+            nflip = int(np.sum(dw > 2e-3))
+            assert nflip <= max(1, int(0.005 * idx.shape[0])), (f, nflip, np.sort(dw)[-5:])
+            flips += nflip
+            worst_w = max(worst_w, float(np.sort(dw)[-nflip - 1]) if nflip < dw.shape[0] else 0.0)
+    finally:
+        eng.close()
+    print(f"{name}: {N_SAMPLES} slots x 3 frames: max |pose - oracle| {worst_p:.3e}, max |w - oracle| {worst_w:.3e} "
+          f"(gate flips excluded: {flips})")

@@ -129,3 +129,46 @@ def test_owners_c4_size():
     b = _run(cfg.N, st.markers, st.K, pf.STATE_F16, pf.RNG_PHILOX, prior, frames, pf.DIAG_BLOCK_RESAMPLE, read=read)
     assert a[1]["out"]["iters"] == 80
     _assert_same(a, b)
+
+
+@pytest.mark.parametrize("state", [pf.STATE_F16, pf.STATE_F32])
+def test_owners_batch_equals_block_resample(state):
+    """Batches (pfmpe_step_multi): k_resample_owners_multi against k_resample_multi, three streams of different N
+    (a partial last block, an occluded stream with 80 iterations), 3 frames, every output of every stream."""
+    sizes = [300_001, 77_777, 1_000_000]
+    streams = [syn.make_stream(syn.StreamConfig("t", M=5, B=50, N=N, seed=21 + i), 3) for i, N in enumerate(sizes)]
+    results = []
+    for diag in (0, pf.DIAG_BLOCK_RESAMPLE):
+        engs = []
+        try:
+            for st, N in zip(streams, sizes):
+                e = make_engine(N, st.markers, st.K, state, pf.RNG_PHILOX, fused=0)
+                e.set_option(pf.OPT_DIAG, diag)
+                e.set_prior(st.prior(fast=True))
+                engs.append(e)
+            snaps = []
+            for f in range(3):
+                ins = []
+                for i, (e, st) in enumerate(zip(engs, streams)):
+                    fr = st.frames[f]
+                    blobs = fr.blobs
+                    if i == 1 and f == 1:  # LED 0 hidden in one stream: 80 iterations, later rounds a subset
+                        uv0 = syn.project(st.K, fr.truth, st.markers)[0]
+                        blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
+                    ins.append(e.make_frame(fr.current_pose, fr.predicted_pose, fr.prediction, blobs=blobs, dt=fr.dt,
+                                            seed=700 + 5 * i + f, frame_idx=f))
+                outs = pf.Engine.step_multi(engs, ins)
+                row = []
+                for e, o in zip(engs, outs):
+                    snap = {"out": o.as_dict(), "w": e.get_weights(), "p1": e.get_particles(1)}
+                    if snap["out"]["resampled"]:
+                        snap["counts"] = e.get_counts()
+                    row.append(snap)
+                snaps.append(row)
+            results.append(snaps)
+        finally:
+            for e in engs:
+                e.close()
+    assert results[0][1][1]["out"]["iters"] == 80
+    for a, b in zip(*results):
+        _assert_same(a, b)
