@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--single-steps", type=int, default=100, help="timed frames per --single-points config")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
+    ap.add_argument("--resident", type=int, default=0, choices=[0, 1],
+                    help="flat one-launch frames through the resident frame server (PFMPE_OPT_RESIDENT)")
     return ap.parse_args()
 
 
@@ -450,6 +452,7 @@ def main():
     eng.set_params(prm)
     eng.set_prior(st.prior())
     eng.set_option(pf.OPT_FUSED, args.fused)
+    eng.set_option(pf.OPT_RESIDENT, args.resident)
     eng.set_option(pf.OPT_PRUNE, args.prune)
     if args.keep_prop >= 0:
         eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
@@ -579,6 +582,9 @@ def main():
         timed = {k: v for k, v in stats.items() if v[0] > 0}
         if shape == pf.SHAPE_FRAME2 and "k_frame" in timed:  # PFMPE_K_FRAME times whichever one-launch kernel ran
             timed["k_frame2"] = timed.pop("k_frame")
+        if shape == pf.SHAPE_RESIDENT and "k_frame" in timed:  # the server's frames: k_frame2's body, device-timed
+            timed["k_frame2_srv"] = timed.pop("k_frame")
+            ab["k_frame2_srv"] = ab["k_frame2"]
         wname = {pf.WEIGH_STREAM: "k_weigh_stream", pf.WEIGH_PK: "k_weigh_pk"}.get(weigh_pass)
         if wname and "k_propagate_weigh" in timed:  # the streaming / packed weighing passes
             timed[wname] = timed.pop("k_propagate_weigh")

@@ -345,11 +345,15 @@ template <>
 __device__ __forceinline__ __half buf_ld<__half>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
   return __ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
 }
+// cache policy of a vector memory access: 16 = sc1 (a store writes through and drops the line from the XCD's L2)
+constexpr int kPolSc1 = 16;
+template <int POL = 0>
 __device__ __forceinline__ void buf_st(float v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, voff, soff, POL);
 }
+template <int POL = 0>
 __device__ __forceinline__ void buf_st(__half v, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  __builtin_amdgcn_raw_buffer_store_b16(__half_as_ushort(v), r, voff, soff, 0);
+  __builtin_amdgcn_raw_buffer_store_b16(__half_as_ushort(v), r, voff, soff, POL);
 }
 
 // fp16 state layout (PFMPE_F16_PAIRS, default 1): planes 2j and 2j + 1 interleaved as ONE plane of 32-bit pairs,
@@ -397,22 +401,29 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
     for (int q = 0; q < 12; ++q) v[q] = base[(int64_t)q * ld + n];
   }
 }
-// store 12 raw state values as particle k
-template <typename SP>
+// store 12 raw state values as particle k (WT: write-through, sc1: the resident server's new prior, read by
+// other workgroups in its next frame without a release fence; MI355X_MICROARCH.md "Valid forms")
+template <typename SP, bool WT = false>
 __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t ld, int k, const SP* v) {
+  constexpr int pol = WT ? kPolSc1 : 0;
   if constexpr (f16_pairs<SP>()) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t pps = (uint32_t)(ld * 4);
 #pragma unroll
     for (int p = 0; p < 6; ++p) {
       const uint32_t w = (uint32_t)__half_as_ushort(v[2 * p]) | ((uint32_t)__half_as_ushort(v[2 * p + 1]) << 16);
-      __builtin_amdgcn_raw_buffer_store_b32(w, r, (uint32_t)k * 4u, (uint32_t)p * pps, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(w, r, (uint32_t)k * 4u, (uint32_t)p * pps, pol);
     }
   } else if constexpr (BufPlanes<SP>::value) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
 #pragma unroll
-    for (int q = 0; q < 12; ++q) buf_st(v[q], r, (uint32_t)k * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+    for (int q = 0; q < 12; ++q) buf_st<pol>(v[q], r, (uint32_t)k * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+  } else if constexpr (WT) {
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      __hip_atomic_store((__attribute__((address_space(1))) SP*)(base + (int64_t)q * ld + k), v[q], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   } else {
 #pragma unroll
     for (int q = 0; q < 12; ++q) base[(int64_t)q * ld + k] = v[q];
@@ -3226,7 +3237,7 @@ struct ResampleLds {
 // finishes the frame.  MODE 2 (k_frame2): the same candidate, then a flat arrival on the sharded count
 // counters; block 0 waits for all of them and finishes.  MODE 0 (k_resample) the block only stores its
 // count partial; k_resample_final finishes.
-template <typename T, int RNG, int MAXM, typename SP, int MODE, bool RAW = false>
+template <typename T, int RNG, int MAXM, typename SP, int MODE, bool RAW = false, bool WT = false>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
@@ -3438,7 +3449,7 @@ __device__ __forceinline__ void resample_phase(
           const auto& row = rows[own];
 #pragma unroll
           for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
-          store_state_raw<SP>(post, fa.ld, k, v);
+          store_state_raw<SP, WT>(post, fa.ld, k, v);
         }
       }
     }
@@ -3911,7 +3922,8 @@ k_resample_owners(const FrameArgsT<T> fa, const Ctrl* __restrict__ ctrl, const S
                   const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
                   const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan,
                   uint32_t* __restrict__ counts, double* __restrict__ mlpose, unsigned long long* __restrict__ winkey) {
-  __shared__ OwnersLds<T> sh;
+  __shared__ OwnersLds<T> shw[kWaves];  // per wave: a batch's waves of one workgroup may be different streams
+  OwnersLds<T>& sh = shw[wave_id_u()];
   const int blk = (int)blockIdx.x * kWaves + wave_id_u();
   if (blk >= fa.nblk) return;
   const Ctrl c = *ctrl;
@@ -3937,7 +3949,9 @@ template <typename T, int RNG, typename SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_OWNERS_MIN_WAVES))) void
 k_resample_owners_multi(const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S,
                         const uint32_t* __restrict__ status, uint32_t gen, int total) {
-  __shared__ OwnersLds<T> sh;
+  __shared__ OwnersLds<T> shw[kWaves];  // per wave: the workgroup's waves may belong to different streams, each
+                                         // staging its own stream's constants for its most-likely particle
+  OwnersLds<T>& sh = shw[wave_id_u()];
   const int gb = (int)blockIdx.x * kWaves + wave_id_u();
   if (gb >= total) return;
   const int s = __builtin_amdgcn_readfirstlane((int)bmap[gb]);
@@ -4454,8 +4468,8 @@ struct Frame2Shared {
 };
 // One frame of k_frame2 for this block.  fa_words: the frame arguments as words (the kernarg segment, or the
 // server's ring slot) for the LDS constants.  Returns false when the block gave up at the weighing barrier's
-// bound (an abandoned frame: no record).
-template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
+// bound (an abandoned frame: no record).  WT: the new prior is stored write-through (the resident server).
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP, bool WT = false>
 __device__ __forceinline__ bool frame2_body(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1,
@@ -4643,8 +4657,9 @@ __device__ __forceinline__ bool frame2_body(
   if (valid) wd = have_P ? (double)w : (double)(kslot ? w1 : w0)[n];
   const BlockScan bs = fl.bs[kslot];
   const GroupScan gs = fl.gs;
-  resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec, tb, cand,
-                                      mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq, stamps, flat, blk);
+  resample_phase<T, RNG, MAXM, SP, 2, false, WT>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec,
+                                                 tb, cand, mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq,
+                                                 stamps, flat, blk);
   return true;
 }
 
@@ -4670,9 +4685,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
 //  * Block 0's wave 0 polls the doorbell (system-scope loads of host memory), copies the message into ring slot j
 //    of device memory (one slot per frame of this dispatch: the scalar cache holds no line of a slot before its
 //    frame, so the frame's arguments can be read with scalar loads, as kernel arguments are) and publishes j + 1
-//    on a device word (release).
-//  * Every block's wave 0 polls that word (agent scope), the block takes an agent-scope acquire (its L1 lines of
-//    last frame's buffers are dropped, as a new dispatch would), and runs frame2_body on the slot.
+//    (write-through) on a device word, once every block has arrived on the done counter (dseq[1]) after the
+//    previous frame.
+//  * Every block's wave 0 polls that word and the done counter, takes ONE agent-scope acquire for the block (its
+//    L1 lines of last frame's buffers are dropped, as a new dispatch would), and the block runs frame2_body on the
+//    slot.  The frame reads as its prior the post set other blocks wrote in the previous frame: those stores are
+//    write-through (sc1) and drained before each block's arrival on the done counter, so no release fence
+//    (MI355X_MICROARCH.md "Valid forms": a release per block wrote back the XCD's whole dirty L2 each time; with
+//    one per wave the frame took 98 us instead of k_frame2's 30).
 //  * Every wait is bounded: the doorbell by idle_ticks (then the server exits by itself; the host restarts it
 //    before that can matter, pfmpe_ctx.hpp kSrvIdleNs), the slot word by the same bound, the frame's own barriers
 //    by its wait bound.  A frame abandoned at a barrier sets the exit bit, so every block returns; the host then
@@ -4684,9 +4704,9 @@ struct alignas(256) SrvMsg {
   const unsigned char* table;  // the frame's blob table in device memory (bank), or null: inline, after the message
   const SP* prior;
   SP* post;
-  int32_t seq, exit_;
-  int32_t tinl;  // bytes of the inline table (a multiple of 8; 0: `table`)
-  int32_t pad;
+  int32_t exit_;  // 1: the server's exit (srv_stop); read with tinl as one 8-byte word
+  int32_t tinl;   // bytes of the inline table (a multiple of 8; 0: `table`)
+  int32_t seq, pad;
 };
 // host mailbox layout (pinned): the doorbell, the per-frame device durations, the message (+ inline table)
 constexpr int kSrvSlots = 256;                        // frames per server dispatch (ring slots)
@@ -4712,11 +4732,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   __shared__ int s_exit, s_zero;
   using Msg = SrvMsg<T, SP>;
   static_assert(sizeof(Msg) % 256 == 0, "ring slots on whole lines");
+  static_assert(offsetof(Msg, exit_) % 8 == 0 && offsetof(Msg, tinl) == offsetof(Msg, exit_) + 4, "{exit_, tinl} word");
   auto host_ld = [](const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
   // every test below is wave-uniform by construction (the wave index through an SGPR, LDS flags through
   // readfirstlane): the frame loop's index then stays uniform, and with it the slot address whose words the body
   // reads as scalars
   const int lane = lane_id(), wv = wave_id_u();
+  // every block, wave 0: the done counter (dseq[1]) holds a count of j * gridDim.x, i.e. every block is through
+  // frame j - 1 (bounded; false: expired)
+  auto wait_done = [&](int j, uint64_t t0) {
+    const uint32_t want = (uint32_t)j * gridDim.x;
+    while (__hip_atomic_load(dseq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      if (rt_now() - t0 > (uint64_t)idle_ticks) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+  };
   for (int j = 0; j < nslots; ++j) {
     unsigned char* slot = ring + (size_t)j * slot_bytes;
     uint64_t t0 = 0;
@@ -4734,21 +4765,22 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
       }
       t0 = rt_now();
       int quit = 1;
-      if (ok) {
+      if (ok && j > 0) ok = wait_done(j, t0);  // nobody still stores frame j - 1's post set
+      if (ok) {  // the message into the slot, write-through (other XCDs read it), drained before the slot word
         const uint64_t* src = (const uint64_t*)(host + kSrvMsgOff);
         uint64_t* dst = (uint64_t*)slot;
         constexpr int kW = (int)(sizeof(Msg) / 8);
-        for (int i = lane; i < kW; i += 64) dst[i] = host_ld(src + i);
+        for (int i = lane; i < kW; i += 64) st_wt(dst + i, host_ld(src + i));
         const uint64_t ex = host_ld(src + offsetof(Msg, exit_) / 8);  // {exit_, tinl}
         quit = (int)(uint32_t)ex;
         const int tw = (int)(uint32_t)(ex >> 32) / 8;
-        for (int i = lane; i < tw; i += 64) dst[kW + i] = host_ld(src + kW + i);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot is in L2 before its word
+        for (int i = lane; i < tw; i += 64) st_wt(dst + kW + i, host_ld(src + kW + i));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       if (lane == 0)
-        __hip_atomic_store(dseq, (uint32_t)(j + 1) | (quit ? kSrvExit : 0u), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(dseq, (uint32_t)(j + 1) | (quit ? kSrvExit : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (wv == 0) {  // every block: the slot's word (bounded as the doorbell, plus a margin)
+    if (wv == 0) {  // every block: the slot's word (bounded as the doorbell, plus a margin), then the done count
       const uint64_t start = rt_now();
       uint32_t v;
       for (;;) {
@@ -4760,6 +4792,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      if (!(v & kSrvExit) && j > 0 && !wait_done(j, start)) v = kSrvExit;
+      // ONE acquire for the block (its L1 lines of the previous frame's buffers dropped, as at a dispatch), drained
+      // before the barrier the other waves pass
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) {
         s_exit = (v & kSrvExit) ? 1 : 0;
         s_zero = (int)(v & 0u);  // 0, through LDS: the slot's address depends on the wait (below)
@@ -4767,7 +4804,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     }
     __syncthreads();
     if (__builtin_amdgcn_readfirstlane(s_exit)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // as a new dispatch: no L1 line of last frame's buffers
     // The slot's words as CONSTANT memory (scalar loads, SGPR operands, as kernel arguments): correct because the
     // slot is written once per dispatch (the scalar cache holds none of its lines before this frame) and before
     // its word is published; the address depends on the LDS word read after the wait, so no load moves above it.
@@ -4775,9 +4811,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     const CMsg* mc = (const CMsg*)(ring_c + (size_t)j * slot_bytes + __builtin_amdgcn_readfirstlane(s_zero));
     const Msg* m = (const Msg*)mc;
     const unsigned char* table = m->tinl ? slot + sizeof(Msg) : m->table;
-    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP>(m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post, w0,
-                                                         w1, part0, part1, ctrl, cpart, flat, counts, cand, mlpose, out,
-                                                         m->seq, stamps, smem, S2);
+    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP, true>(m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post,
+                                                               w0, w1, part0, part1, ctrl, cpart, flat, counts, cand,
+                                                               mlpose, out, m->seq, stamps, smem, S2);
     if (!__builtin_amdgcn_readfirstlane((int)ok)) {
       if (threadIdx.x == 0) __hip_atomic_fetch_or(dseq, kSrvExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;  // abandoned at a barrier: every block leaves (the host redoes the frame with launches)
@@ -4785,6 +4821,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     if (blockIdx.x == 0 && threadIdx.x == 0)  // the frame's device time: doorbell seen -> block 0 done (record out)
       __hip_atomic_store((uint64_t*)(host + kSrvDurOff) + j, rt_now() - t0, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+    // the block's end of frame: every wave's stores drained (the post set went write-through), then ONE arrival
+    // on the done counter for the block (MI355X_MICROARCH.md "Valid forms", row 1; no release fence, which would
+    // write back the XCD's whole dirty L2 once per block)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(dseq + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

@@ -90,7 +90,7 @@ void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart, c->d_winkey,
                  c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
-                 c->d_stamps, c->d_owner[0], c->d_owner[1]};
+                 c->d_stamps, c->d_owner[0], c->d_owner[1], c->d_srv, c->d_srv_seq};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -98,6 +98,7 @@ void free_all(pfmpe_ctx* c) {
   c->h_out = nullptr;
   if (c->h_table) (void)hipHostFree(c->h_table);
   if (c->h_det) (void)hipHostFree(c->h_det);
+  if (c->h_srv) (void)hipHostFree(c->h_srv);
   for (auto& e : c->ev_pool) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -277,6 +278,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
 void pfmpe_destroy(pfmpe_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  (void)srv_stop(c);  // the resident server's exit message, else the stream drains only at its idle bound
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->last_fence) (void)hipEventSynchronize(c->last_fence->ev);  // a batch led by another context
   c->last_fence.reset();
@@ -355,6 +357,11 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
       return PFMPE_OK;
     case PFMPE_OPT_DEFER_RESAMPLE:
       c->defer = value != 0;
+      return PFMPE_OK;
+    case PFMPE_OPT_RESIDENT:
+      if (value < 0 || value > 1) return fail(c, PFMPE_E_ARG, "set_option: RESIDENT is 0 or 1");
+      c->resident = value != 0;
+      if (!c->resident) RET(set_device(c));  // ends a running server
       return PFMPE_OK;
     case PFMPE_OPT_MULTI_MAX_BLOCKS:
       if (value < 1 || value > kMultiMaxBlocks) return fail(c, PFMPE_E_ARG, "set_option: MULTI_MAX_BLOCKS is 1 .. 160000");
@@ -475,7 +482,8 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
 
 int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   RET(check_step(c, in, out));
-  RET(set_device(c));
+  RET(set_device(c, /*keep_server=*/true));  // the frame's own path stops it if it launches (Seq::step)
+  c->tbl_pending = false;
   const unsigned char* table = c->d_table;
   const int B = in->B;
   size_t tbytes = 0;
@@ -488,7 +496,12 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     // the x-bucketed table is built here, O(B), and travels in the same copy the blobs would
     tbytes = build_table(c, in->blobs, B, c->h_table);
     gh = *(const GridHdr*)(c->h_table + grid_off(c, B));
-    HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
+    if (c->resident) {  // a served frame takes it inline in its message; a launched one copies it (stage_host_table)
+      c->tbl_pending = true;
+      c->tbl_bytes = tbytes;
+    } else {
+      HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
+    }
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
   const size_t ev_mark = c->ev_used;  // brackets of earlier frames still pending (harvested lazily)
@@ -754,6 +767,10 @@ int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
 
 int pfmpe_get_kernel_stats(pfmpe_ctx* c, int kernel, int64_t* launches, double* total_ms) {
   if (!c || kernel < 0 || kernel >= PFMPE_K_COUNT) return PFMPE_E_ARG;
+  if (c->srv_alive) {  // the resident server's frame durations are read once it has ended
+    HIPCHK(c, hipSetDevice(c->device));
+    RET(srv_stop(c));
+  }
   if (c->ev_used) {  // pending brackets of timed frames
     HIPCHK(c, hipSetDevice(c->device));
     RET(harvest_timing(c));
@@ -773,12 +790,18 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case PFMPE_INFO_LAST_GRID: *value = c->last_grid; return PFMPE_OK;
     case PFMPE_INFO_GUARD_SKIPS: *value = c->guard_skips; return PFMPE_OK;
     case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
+    case PFMPE_INFO_SERVER_DISPATCHES: *value = c->srv_dispatches; return PFMPE_OK;
+    case PFMPE_INFO_SERVER_FRAMES: *value = c->srv_frames; return PFMPE_OK;
     default: return PFMPE_E_ARG;
   }
 }
 
 int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
   if (!c) return PFMPE_E_ARG;
+  if (c->srv_alive) {  // its timed frames belong to the statistics being reset
+    HIPCHK(c, hipSetDevice(c->device));
+    RET(srv_stop(c));
+  }
   if (c->ev_used) {  // pending brackets belong to the statistics being reset
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].b));  // before their events are recorded again
