@@ -335,15 +335,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const SP* base, int
   const uint32_t bytes = (uint32_t)(12 * ld * (int64_t)sizeof(SP));
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
-template <typename SP>
-__device__ __forceinline__ SP buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff);
-template <>
-__device__ __forceinline__ float buf_ld<float>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-template <>
-__device__ __forceinline__ __half buf_ld<__half>(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  return __ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0));
+template <typename SP, int POL = 0>
+__device__ __forceinline__ SP buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  if constexpr (std::is_same<SP, float>::value)
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, POL));
+  else
+    return __ushort_as_half(__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, POL));
 }
 // cache policy of a vector memory access: 16 = sc1 (a store writes through and drops the line from the XCD's L2)
 constexpr int kPolSc1 = 16;
@@ -379,15 +376,16 @@ __host__ __device__ __forceinline__ int64_t plane_index(int q, int64_t n, int64_
     return (int64_t)q * ld + n;
 }
 
-// the 12 state values of particle n of a state buffer (raw SP values, no anchor / conversion)
-template <typename SP>
+// the 12 state values of particle n of a state buffer (raw SP values, no anchor / conversion).  POL kPolSc1: the
+// loads bypass L1 (the resident server's prior, written write-through by other workgroups in its previous frame)
+template <typename SP, int POL = 0>
 __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int64_t ld, int n, SP* v) {
   if constexpr (f16_pairs<SP>()) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
     const uint32_t pps = (uint32_t)(ld * 4);
 #pragma unroll
     for (int p = 0; p < 6; ++p) {
-      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)p * pps, 0);
+      const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (uint32_t)n * 4u, (uint32_t)p * pps, POL);
       v[2 * p] = __ushort_as_half((unsigned short)(w & 0xffffu));
       v[2 * p + 1] = __ushort_as_half((unsigned short)(w >> 16));
     }
@@ -395,7 +393,12 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
     const __amdgpu_buffer_rsrc_t r = plane_rsrc(base, ld);
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
 #pragma unroll
-    for (int q = 0; q < 12; ++q) v[q] = buf_ld<SP>(r, (uint32_t)n * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+    for (int q = 0; q < 12; ++q) v[q] = buf_ld<SP, POL>(r, (uint32_t)n * (uint32_t)sizeof(SP), (uint32_t)q * ps);
+  } else if constexpr (POL != 0) {
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      v[q] = __hip_atomic_load((const __attribute__((address_space(1))) SP*)(base + (int64_t)q * ld + n),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   } else {
 #pragma unroll
     for (int q = 0; q < 12; ++q) v[q] = base[(int64_t)q * ld + n];
@@ -523,10 +526,10 @@ template <typename T>
 __device__ __forceinline__ int prior_row(const FrameArgsT<T>& fa, int n) {
   return fa.owner ? (int)fa.owner[n] : n;
 }
-template <typename T, typename SP>
+template <typename T, typename SP, int POL = 0>
 __device__ __forceinline__ void load_prior(const FrameArgsT<T>& fa, const SP* __restrict__ prior, int n, T* A) {
   SP v[12];
-  load_state_raw<SP>(prior, fa.ld, prior_row(fa, n), v);
+  load_state_raw<SP, POL>(prior, fa.ld, prior_row(fa, n), v);
 #pragma unroll
   for (int q = 0; q < 12; ++q) A[q] = StateIO<T, SP>::load(v[q], fa.anc_in[q]);
 }
@@ -4490,7 +4493,7 @@ __device__ __forceinline__ bool frame2_body(
 
   copy_table(table, smem, (size_t)fa.tbytes);
   T A[12];
-  if (valid && n >= 2) load_prior(fa, prior, n, A);
+  if (valid && n >= 2) load_prior<T, SP, WT ? kPolSc1 : 0>(fa, prior, n, A);
   stage_consts_from(fa_words, sc);
   if (threadIdx.x == 0) {
     fl.c = zero_ctrl();  // start of frame: every block keeps an identical copy of the control record
@@ -4685,14 +4688,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
 //  * Block 0's wave 0 polls the doorbell (system-scope loads of host memory), copies the message into ring slot j
 //    of device memory (one slot per frame of this dispatch: the scalar cache holds no line of a slot before its
 //    frame, so the frame's arguments can be read with scalar loads, as kernel arguments are) and publishes j + 1
-//    (write-through) on a device word, once every block has arrived on the done counter (dseq[1]) after the
+//    (write-through) on a device word, once every block has arrived on the done counter (dseq[kSrvDoneOff]) after the
 //    previous frame.
-//  * Every block's wave 0 polls that word and the done counter, takes ONE agent-scope acquire for the block (its
-//    L1 lines of last frame's buffers are dropped, as a new dispatch would), and the block runs frame2_body on the
-//    slot.  The frame reads as its prior the post set other blocks wrote in the previous frame: those stores are
-//    write-through (sc1) and drained before each block's arrival on the done counter, so no release fence
-//    (MI355X_MICROARCH.md "Valid forms": a release per block wrote back the XCD's whole dirty L2 each time; with
-//    one per wave the frame took 98 us instead of k_frame2's 30).
+//  * Every block's wave 0 polls that word and the done counter, and the block runs frame2_body on the slot.  The
+//    frame reads as its prior the post set other blocks wrote in the previous frame: those stores are write-through
+//    (sc1) and drained before each block's arrival on the done counter, and the prior loads are sc1 loads, so
+//    neither side fences (MI355X_MICROARCH.md "Valid forms", row 1; a release per wave, which writes back the
+//    XCD's whole dirty L2 each time, had the frame take 98 us instead of k_frame2's 30).  Block 0 alone takes an
+//    acquire (its final phase regenerates the winner from the prior with plain loads).
 //  * Every wait is bounded: the doorbell by idle_ticks (then the server exits by itself; the host restarts it
 //    before that can matter, pfmpe_ctx.hpp kSrvIdleNs), the slot word by the same bound, the frame's own barriers
 //    by its wait bound.  A frame abandoned at a barrier sets the exit bit, so every block returns; the host then
@@ -4704,6 +4707,21 @@ struct alignas(256) SrvMsg {
   const unsigned char* table;  // the frame's blob table in device memory (bank), or null: inline, after the message
   const SP* prior;
   SP* post;
+  // k_frame2's buffers, per message although fixed for a dispatch: read from the slot where the frame uses them
+  // (scalar loads), they are not live across the server's frame loop (as kernel arguments they were hoisted out of
+  // it and spilled)
+  T* w0;
+  T* w1;
+  BlockPart* part0;
+  BlockPart* part1;
+  Ctrl* ctrl;
+  CountPart* cpart;
+  uint32_t* flat;
+  uint32_t* counts;
+  Cand* cand;
+  double* mlpose;
+  RecOut* out;
+  uint64_t* stamps;
   int32_t exit_;  // 1: the server's exit (srv_stop); read with tinl as one 8-byte word
   int32_t tinl;   // bytes of the inline table (a multiple of 8; 0: `table`)
   int32_t seq, pad;
@@ -4713,20 +4731,30 @@ constexpr int kSrvSlots = 256;                        // frames per server dispa
 constexpr size_t kSrvDurOff = 256;                    // uint64 dur[kSrvSlots]: s_memrealtime ticks, frame j
 constexpr size_t kSrvMsgOff = kSrvDurOff + 8 * kSrvSlots;
 constexpr uint32_t kSrvExit = 0x80000000u;            // the slot word's exit bit
+constexpr int kSrvDoneOff = 32;                       // dseq[32]: the done counter, 128 B from the slot word
+// Between frames every block's wave 0 polls the slot word: ~0.43 us apart (1,024 cycles), not back to back.  With
+// s_sleep 1 the 390 idle pollers of C2 hammered one line while the frame's last phase ran (the final block took
+// 8 us instead of 1: MI355X_MICROARCH.md, pollers cut chip bandwidth)
+#ifndef PFMPE_SRV_POLL_SLEEP
+#define PFMPE_SRV_POLL_SLEEP 16
+#endif
+constexpr int kSrvPollSleep = PFMPE_SRV_POLL_SLEEP;
 
 // 3 waves per SIMD: two resident blocks per CU next to the occupancy margin, as a one-launch k_frame2 needs
 // (pfmpe_ctx.hpp frame_fused); unconstrained, the frame loop's live state took the server past 168 VGPRs
 #ifndef PFMPE_FRAME2_SRV_MIN_WAVES
 #define PFMPE_FRAME2_SRV_MIN_WAVES 3
 #endif
+// 1: the server's new prior is stored write-through (no release fence per block); 0 (A/B): plain stores and one
+// release fence per block at the end of the frame
+#ifndef PFMPE_SRV_WT
+#define PFMPE_SRV_WT 1
+#endif
 template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_SRV_MIN_WAVES))) void k_frame2_srv(
     const unsigned char* __restrict__ host, unsigned char* __restrict__ ring,
     const __attribute__((address_space(4))) unsigned char* ring_c, uint32_t slot_bytes, int nslots,
-    uint32_t* __restrict__ dseq, uint32_t idle_ticks, T* __restrict__ w0, T* __restrict__ w1,
-    BlockPart* __restrict__ part0, BlockPart* __restrict__ part1, Ctrl* __restrict__ ctrl,
-    CountPart* __restrict__ cpart, uint32_t* __restrict__ flat, uint32_t* __restrict__ counts, Cand* __restrict__ cand,
-    double* __restrict__ mlpose, RecOut* __restrict__ out, uint64_t* __restrict__ stamps) {
+    uint32_t* __restrict__ dseq, uint32_t idle_ticks, uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ Frame2Shared<T> S2;
   __shared__ int s_exit, s_zero;
@@ -4738,13 +4766,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   // readfirstlane): the frame loop's index then stays uniform, and with it the slot address whose words the body
   // reads as scalars
   const int lane = lane_id(), wv = wave_id_u();
-  // every block, wave 0: the done counter (dseq[1]) holds a count of j * gridDim.x, i.e. every block is through
-  // frame j - 1 (bounded; false: expired)
+  uint32_t* done = dseq + kSrvDoneOff;  // the done counter, on a line of its own
+  // every block, wave 0: the done counter holds a count of j * gridDim.x, i.e. every block is through frame j - 1
+  // (bounded; false: expired)
   auto wait_done = [&](int j, uint64_t t0) {
     const uint32_t want = (uint32_t)j * gridDim.x;
-    while (__hip_atomic_load(dseq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
       if (rt_now() - t0 > (uint64_t)idle_ticks) return false;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(kSrvPollSleep);
     }
     return true;
   };
@@ -4766,19 +4795,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
       t0 = rt_now();
       int quit = 1;
       if (ok && j > 0) ok = wait_done(j, t0);  // nobody still stores frame j - 1's post set
-      if (ok) {  // the message into the slot, write-through (other XCDs read it), drained before the slot word
+      if (ok) {  // the message into the slot, write-through (other XCDs read it), drained before the slot word.
+                 // Every host read of a round is issued before the first is used (one PCIe round trip per round)
         const uint64_t* src = (const uint64_t*)(host + kSrvMsgOff);
         uint64_t* dst = (uint64_t*)slot;
         constexpr int kW = (int)(sizeof(Msg) / 8);
-        for (int i = lane; i < kW; i += 64) st_wt(dst + i, host_ld(src + i));
-        const uint64_t ex = host_ld(src + offsetof(Msg, exit_) / 8);  // {exit_, tinl}
+        constexpr int kR = (kW + 63) / 64;
+        static_assert(kR <= 8, "message words per lane");
+        uint64_t wv8[kR];
+#pragma unroll
+        for (int r = 0; r < kR; ++r) wv8[r] = (lane + 64 * r < kW) ? host_ld(src + lane + 64 * r) : 0ull;
+#pragma unroll
+        for (int r = 0; r < kR; ++r)
+          if (lane + 64 * r < kW) st_wt(dst + lane + 64 * r, wv8[r]);
+        constexpr int kEx = (int)(offsetof(Msg, exit_) / 8);  // {exit_, tinl}
+        const uint64_t ex = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wv8[kEx / 64], kEx % 64) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wv8[kEx / 64] >> 32), kEx % 64)
+                             << 32);
         quit = (int)(uint32_t)ex;
         const int tw = (int)(uint32_t)(ex >> 32) / 8;
-        for (int i = lane; i < tw; i += 64) st_wt(dst + kW + i, host_ld(src + kW + i));
+        for (int i = lane; i < tw; i += 256) {  // the inline table, four reads in flight per lane
+          uint64_t t4[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) t4[r] = (i + 64 * r < tw) ? host_ld(src + kW + i + 64 * r) : 0ull;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (i + 64 * r < tw) st_wt(dst + kW + i + 64 * r, t4[r]);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       if (lane == 0)
         __hip_atomic_store(dseq, (uint32_t)(j + 1) | (quit ? kSrvExit : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (stamps && lane == 0) {  // diagnostic: doorbell seen, slot published (row 0, single writer)
+        stamps[4] = t0;
+        stamps[30] = rt_now();
+      }
     }
     if (wv == 0) {  // every block: the slot's word (bounded as the doorbell, plus a margin), then the done count
       const uint64_t start = rt_now();
@@ -4790,13 +4841,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
           v = kSrvExit;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(kSrvPollSleep);
       }
       if (!(v & kSrvExit) && j > 0 && !wait_done(j, start)) v = kSrvExit;
-      // ONE acquire for the block (its L1 lines of the previous frame's buffers dropped, as at a dispatch), drained
-      // before the barrier the other waves pass
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // The prior loads of the frame body bypass L1 (sc1, WT), so a block needs no acquire for them; block 0 takes
+      // ONE (its finalize regenerates the winner from the prior with plain loads), drained before the barrier
+      if (blockIdx.x == 0 || PFMPE_SRV_WT == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       if (lane == 0) {
         s_exit = (v & kSrvExit) ? 1 : 0;
         s_zero = (int)(v & 0u);  // 0, through LDS: the slot's address depends on the wait (below)
@@ -4811,9 +4864,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     const CMsg* mc = (const CMsg*)(ring_c + (size_t)j * slot_bytes + __builtin_amdgcn_readfirstlane(s_zero));
     const Msg* m = (const Msg*)mc;
     const unsigned char* table = m->tinl ? slot + sizeof(Msg) : m->table;
-    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP, true>(m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post,
-                                                               w0, w1, part0, part1, ctrl, cpart, flat, counts, cand,
-                                                               mlpose, out, m->seq, stamps, smem, S2);
+    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP, PFMPE_SRV_WT != 0>(
+        m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post, m->w0, m->w1, m->part0, m->part1, m->ctrl, m->cpart,
+        m->flat, m->counts, m->cand, m->mlpose, m->out, m->seq, m->stamps, smem, S2);
     if (!__builtin_amdgcn_readfirstlane((int)ok)) {
       if (threadIdx.x == 0) __hip_atomic_fetch_or(dseq, kSrvExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;  // abandoned at a barrier: every block leaves (the host redoes the frame with launches)
@@ -4826,7 +4879,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
     // write back the XCD's whole dirty L2 once per block)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(dseq + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+      // plain post stores (A/B build): one release for the block.  Diagnostic stamps: written back to memory, where
+      // pfmpe_debug_stamps reads them on a side stream while the server runs
+      if (PFMPE_SRV_WT == 0 || stamps) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

@@ -122,7 +122,7 @@ struct pfmpe_ctx {
   size_t srv_bytes = 0;
   unsigned char* d_srv = nullptr;  // ring: kSrvSlots message slots in HBM
   size_t srv_slot = 0;
-  uint32_t* d_srv_seq = nullptr;   // [slot word, done counter]
+  uint32_t* d_srv_seq = nullptr;   // slot word [0], done counter [kSrvDoneOff] (256 B)
   std::vector<uint8_t> srv_timed;  // per ring slot: a timed frame (its duration goes to PFMPE_K_FRAME)
   int64_t srv_dispatches = 0;
   int64_t srv_frames = 0;
@@ -146,6 +146,7 @@ struct pfmpe_ctx {
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
+  hipStream_t side_stream = nullptr;  // pfmpe_debug_stamps beside a running resident server
   // batch scratch (pfmpe_step_multi, owned by the batch's first context): stream descriptors, the
   // block -> stream map and host-supplied blob tables; the host writes the descriptors and tables into the
   // pinned image, a staging launch (k_stage_multi) moves them to HBM and builds the map
@@ -775,12 +776,11 @@ struct Seq {
         c->srv_slot = slot;
       }
       std::memset(c->h_srv, 0, kSrvMsgOff);  // doorbell 0, durations
-      HIPCHK(c, hipMemsetAsync(c->d_srv_seq, 0, 2 * sizeof(uint32_t), c->stream));
+      HIPCHK(c, hipMemsetAsync(c->d_srv_seq, 0, 256, c->stream));  // slot word, done counter (kSrvDoneOff)
       typedef const __attribute__((address_space(4))) unsigned char* ConstRing;
       hipLaunchKernelGGL((k_frame2_srv<T, RNG, MAXM, PRUNE, SP>), dim3(fa_in.nblk), dim3(kBlock), lds, c->stream,
                          (const unsigned char*)c->hd_srv, c->d_srv, (ConstRing)c->d_srv, (uint32_t)slot, kSrvSlots,
-                         c->d_srv_seq, kSrvIdleTicks, (T*)c->d_w[0], (T*)c->d_w[1], c->d_part[0], c->d_part[1],
-                         c->d_ctrl, c->d_cpart, c->d_flat, counts, c->d_cand, c->d_mlpose, c->d_out, c->d_stamps);
+                         c->d_srv_seq, kSrvIdleTicks, c->d_stamps);
       HIPCHK(c, hipGetLastError());
       guard.b = nullptr;  // held by the server until srv_stop
       c->srv_alive = true;
@@ -802,6 +802,18 @@ struct Seq {
     std::memcpy((void*)&m->fa, (const void*)&a, sizeof(a));
     m->prior = (const SP*)c->d_state[c->prior_idx];
     m->post = (SP*)c->d_state[1 - c->prior_idx];
+    m->w0 = (T*)c->d_w[0];
+    m->w1 = (T*)c->d_w[1];
+    m->part0 = c->d_part[0];
+    m->part1 = c->d_part[1];
+    m->ctrl = c->d_ctrl;
+    m->cpart = c->d_cpart;
+    m->flat = c->d_flat;
+    m->counts = counts;
+    m->cand = c->d_cand;
+    m->mlpose = c->d_mlpose;
+    m->out = c->d_out;
+    m->stamps = c->d_stamps;
     m->seq = c->seq;
     m->exit_ = 0;
     const bool inl = c->tbl_pending;

@@ -105,6 +105,7 @@ void free_all(pfmpe_ctx* c) {
   }
   if (c->d_multi) (void)hipFree(c->d_multi);
   if (c->h_multi) (void)hipHostFree(c->h_multi);
+  if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -742,16 +743,25 @@ int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
 // Undocumented diagnostic: reset (out == NULL) or read the kStamps stamps of the last frame (diag & 4).
 int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
   if (!c || !c->d_stamps) return PFMPE_E_STATE;
-  RET(set_device(c));
+  // a running resident server keeps the stream: the stamps (written back at each frame's end) go through a side
+  // stream, so steady-state frames can be stamped
+  hipStream_t st = c->stream;
+  if (c->srv_alive) {
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->side_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
+    st = c->side_stream;
+  } else {
+    RET(set_device(c));
+  }
   const size_t rows = 1 + (size_t)c->max_blk;
   if (!out) {
-    HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, rows * kStamps * sizeof(uint64_t), c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, rows * kStamps * sizeof(uint64_t), st));
+    HIPCHK(c, hipStreamSynchronize(st));
     return PFMPE_OK;
   }
   std::vector<uint64_t> h(rows * kStamps);
-  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->d_stamps, h.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(c, hipStreamSynchronize(st));
   for (int i = 0; i < kStamps; ++i) {
     const bool is_min = i == 0 || i == 4 || i == 19;
     uint64_t v = h[i];
