@@ -117,7 +117,8 @@ struct FrameArgsT {
   uint32_t wait_ticks;            // bound of every in-launch wait, s_memrealtime ticks (100 MHz)
   uint32_t flat_base_w, flat_base_c;  // k_frame2: running totals of the flat counter sets at frame start
   int32_t tbytes;                 // this frame's blob table, bytes (base + grid: build_blob_table_host)
-  int32_t pad_fa;
+  uint32_t gtag;                  // k_frame2: this frame's granule tag base (frame << 12; the iteration in the low
+                                  // 12 bits), never 0 (pfmpe_ctx.hpp next_gtag)
   GridArgs grid;                  // the table's 2D grid (fp32 pruned column minima)
   int64_t ld;                     // SoA plane stride in elements
   T anc_in[12], anc_out[12];      // fp16 state only: anchors of the prior / of the new prior
@@ -1692,6 +1693,29 @@ __device__ __forceinline__ bool flat_wait(const uint32_t* set, uint32_t target, 
   }
 }
 
+
+// ---- granule hand-offs (MI355X_MICROARCH.md / cdna_hip_programming.md Guideline 16 R2): the data IS the flag.  A
+// 32-bit payload word travels in an 8-byte {payload, tag} granule written by ONE aligned write-through (sc1) store;
+// the consumer re-reads granules (sc1 loads) until every tag equals the one it expects: no arrival counter, no
+// drain before it, no separate load round.  Used for the flat count barrier (block 0 alone polls 2 granules per
+// block).  Tags are unique per frame (FrameArgsT::gtag); the host zeroes the area at create and when its frame
+// count wraps, so a stale word never carries a live tag.  (The weighing barrier keeps its counter: there every
+// block reads every partial, and polling 391 blocks x 96 B of granules from every block hammered the fabric: the
+// barrier took 20 us instead of 5 at C2, profiles/r05/granule_weighing_rejected.txt.)
+// The flat path's area: the two parities of block partials (BlockPart, k_frame2's weighing barrier), then the count
+// granules {count, index} of up to kFlatMaxGroups * kGroup blocks.
+constexpr size_t kGranPartBytes = (size_t)kFlatMaxGroups * kGroup * sizeof(BlockPart);  // per parity
+constexpr size_t kGranCountOff = 2 * kGranPartBytes;
+constexpr size_t kGranBytes = kGranCountOff + (size_t)kFlatMaxGroups * kGroup * 16;
+__device__ __forceinline__ void store_granule(uint64_t* g, uint32_t tag, uint32_t v) {
+  __hip_atomic_store((gu64_t*)g, ((uint64_t)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// two granules as ONE 16-B write-through-coherent (sc1) load: {payload0, tag0, payload1, tag1}
+__device__ __forceinline__ u32x4_t ld_gran2_issue(const uint64_t* p) {
+  u32x4_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"((const char*)p) : "memory");
+  return r;
+}
 
 // ============================================================================== kernels
 // ---- blob table (DESIGN.md "Exact blob pruning"), built once per frame on the host (build_blob_table_host,
@@ -3499,28 +3523,41 @@ __device__ __forceinline__ void resample_phase(
   }
   if (wv != 0) return;
 
-  if (MODE == 2) {  // flat: count partial + one arrival; block 0 waits for every block and finishes
-    if (lane == 0) {
+  if (MODE == 2) {  // flat: the count partial as two granules {count, index}; block 0 polls every block's and finishes
+    {
       int bv = sh.c[0], bi = sh.ci[0];
       for (int w = 1; w < kWaves; ++w) cmb_max(bv, bi, sh.c[w], sh.ci[w]);
-      st_wt(cpart + blk, pack2(bv, bi));
-      if (stamps) stamp_max(stamps, 5, rt_now());
-      flat_arrive(flat + kFlatCountSet, blk);
+      if (lane < 2) store_granule((uint64_t*)cpart + 2 * blk + lane, fa.gtag, (uint32_t)(lane ? bi : bv));
+      if (stamps && lane == 0) stamp_max(stamps, 5, rt_now());
     }
     if (blk != 0) return;
-    if (!flat_wait(flat + kFlatCountSet, fa.flat_base_c + (uint32_t)fa.nblk, fa.wait_ticks)) return;  // abandoned
-    // every count partial of the frame (nblk <= kFlatMaxGroups * kGroup = 8 per lane) requested in ONE round
-    // trip, then combined; a lane past nblk holds the identity (count -1)
+    // every count partial of the frame (nblk <= kFlatMaxGroups * kGroup = 8 per lane), one 16-B load each, all in
+    // flight together, re-read until every tag is this frame's (bounded: abandoned); then combined, a lane past
+    // nblk holding the identity (count -1)
     int bv = -1, bi = 0x7fffffff;
     {
-      uint64_t cp[kFlatMaxGroups];
+      u32x4_t cp[kFlatMaxGroups] = {};
+      const uint64_t t0 = rt_now();
+      for (;;) {
 #pragma unroll
-      for (int j = 0; j < kFlatMaxGroups; ++j) {
-        const int t = lane + 64 * j;
-        cp[j] = t < fa.nblk ? ld_wt(cpart + t) : pack2(-1, 0x7fffffff);
+        for (int j = 0; j < kFlatMaxGroups; ++j) {
+          const int t = lane + 64 * j;
+          cp[j] = ld_gran2_issue((const uint64_t*)cpart + 2 * (t < fa.nblk ? t : 0));
+        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(cp[0]), "+v"(cp[1]), "+v"(cp[2]), "+v"(cp[3]), "+v"(cp[4]), "+v"(cp[5]),
+                     "+v"(cp[6]), "+v"(cp[7])::"memory");
+        static_assert(kFlatMaxGroups == 8, "the wait's operand list");
+        bool stale = false;
+#pragma unroll
+        for (int j = 0; j < kFlatMaxGroups; ++j)
+          stale |= lane + 64 * j < fa.nblk && (cp[j].y != fa.gtag || cp[j].w != fa.gtag);
+        if (!__builtin_amdgcn_ballot_w64(stale)) break;
+        if (rt_now() - t0 > fa.wait_ticks) return;  // abandoned
+        __builtin_amdgcn_s_sleep(1);
       }
 #pragma unroll
-      for (int j = 0; j < kFlatMaxGroups; ++j) cmb_max(bv, bi, lo32(cp[j]), hi32(cp[j]));
+      for (int j = 0; j < kFlatMaxGroups; ++j)
+        if (lane + 64 * j < fa.nblk) cmb_max(bv, bi, (int)cp[j].x, (int)cp[j].z);
     }
     wave_argmax(bv, bi);
     if (stamps && lane == 0) stamps[6] = rt_now();
@@ -4454,11 +4491,11 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
 }
 
 // The flat frame is one launch only while 2 blocks fit per CU next to the occupancy margin (pfmpe_ctx.hpp
-// frame_fused), i.e. 3 waves per SIMD.  fp64 needs the cap stated (it would take 214 VGPRs, 2 waves, and
-// silently fall back to two launches above 256 blocks); the fp64 TUs define it to 3.  fp32/fp16 fit as they
-// are, and an explicit cap there only trades registers for scratch.
+// frame_fused), i.e. 3 waves per SIMD (<= 168 VGPRs).  Without the cap fp64 took 214 VGPRs and fp32 187 once the
+// granule polls kept 12 16-B loads per lane in flight (both would silently fall back to two launches above 256
+// blocks); with it fp32 fits without scratch.
 #ifndef PFMPE_FRAME2_MIN_WAVES
-#define PFMPE_FRAME2_MIN_WAVES 1
+#define PFMPE_FRAME2_MIN_WAVES 3
 #endif
 // The LDS of a k_frame2 block (the one-launch kernel and the resident frame server share the body)
 template <typename T>

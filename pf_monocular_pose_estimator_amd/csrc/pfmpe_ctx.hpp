@@ -95,6 +95,8 @@ struct pfmpe_ctx {
   bool coop = false;               // device supports cooperative launches
   int fused = 2;                   // PFMPE_OPT_FUSED: 2 flat one-launch (k_frame2), 1 tree (k_frame), 0 two launches
   uint32_t* d_flat = nullptr;      // k_frame2 sharded arrival counters (kFlatWords)
+  unsigned char* d_gran = nullptr; // k_frame2 granule hand-offs (kGranBytes: block partials x 2 parities, counts)
+  uint32_t gframe = 0;             // granule tag frame count (1 .. kGranFrames; the area is zeroed on wrap)
   uint32_t flat_base_w = 0, flat_base_c = 0;  // their running totals (host mirror)
   int64_t fused_fallbacks = 0;     // fused frames redone with two launches
   int fused_user = 2;              // the PFMPE_OPT_FUSED value asked for (fused drops to 0 after a fallback)
@@ -126,6 +128,9 @@ struct pfmpe_ctx {
   std::vector<uint8_t> srv_timed;  // per ring slot: a timed frame (its duration goes to PFMPE_K_FRAME)
   int64_t srv_dispatches = 0;
   int64_t srv_frames = 0;
+  // host-side timing of served frames (undocumented info keys 100-102): record -> next doorbell (host work between
+  // frames), doorbell -> record (the frame as the host sees it), frames counted
+  int64_t srv_host_ns = 0, srv_wait_ns = 0, srv_timed_frames = 0, srv_rec_ns = 0;
   bool tbl_pending = false;        // h_table holds this frame's table, not yet copied to d_table (resident mode)
   size_t tbl_bytes = 0;
   Ctrl* d_ctrl = nullptr;
@@ -513,6 +518,23 @@ inline int abandoned(pfmpe_ctx* c) {
            std::string(c->fused_rearm > 0 ? " until PFMPE_OPT_FUSED_REARM clean frames" : "");
   return PFMPE_OK;
 }
+// This flat frame's granule tag base (FrameArgsT::gtag): frame count << 12, never 0.  On wrap the granule area is
+// zeroed first, so no stored word carries a tag a later frame uses (the stream must be free: no server running).
+constexpr uint32_t kGranFrames = 0xFFFFF;
+inline int next_gtag(pfmpe_ctx* c, uint32_t* gtag) {
+  if (c->gframe >= kGranFrames) {
+    HIPCHK(c, hipMemsetAsync(c->d_gran, 0, kGranBytes, c->stream));
+    c->gframe = 0;
+  }
+  c->gframe += 1;
+  *gtag = c->gframe << 12;
+  return PFMPE_OK;
+}
+inline BlockPart* gran_part(const pfmpe_ctx* c, int parity) {
+  return (BlockPart*)(c->d_gran + (size_t)parity * kGranPartBytes);
+}
+inline CountPart* gran_count(const pfmpe_ctx* c) { return (CountPart*)(c->d_gran + kGranCountOff); }
+
 // resident mode leaves a host-supplied table in h_table (the server takes it inline); any launched frame copies it
 inline int stage_host_table(pfmpe_ctx* c) {
   if (!c->tbl_pending) return PFMPE_OK;
@@ -679,6 +701,10 @@ struct Seq {
     FrameArgsT<T> a = fa_in;
     a.flat_base_w = c->flat_base_w;
     a.flat_base_c = c->flat_base_c;
+    // granule tags: k_frame2's hand-offs, and k_frame's count barrier unless it runs as a tree (kDiagTreeCount)
+    // (the flat count barrier's poll covers <= kFlatMaxGroups * kGroup blocks: at most 2 per CU on 256 CUs)
+    const bool tree_count = !flat && ((c->diag & kDiagTreeCount) || a.nblk > kFlatMaxGroups * kGroup);
+    if (!tree_count) RET(next_gtag(c, &a.gtag));
     const SP* prior = (const SP*)c->d_state[c->prior_idx];
     SP* post = (SP*)c->d_state[1 - c->prior_idx];
     T* w0 = (T*)c->d_w[0];
@@ -693,14 +719,15 @@ struct Seq {
     RET(launch_ext(c, PFMPE_K_FRAME, [&] {
       if (flat)
         klaunch(c, k_frame2<T, RNG, MAXM, PRUNE, SP>, dim3(a.nblk), dim3(kBlock), lds, a, table,
-                           prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_ctrl, c->d_cpart, c->d_flat, counts,
-                           c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps);
+                           prior, post, w0, w1, gran_part(c, 0), gran_part(c, 1), c->d_ctrl, gran_count(c), c->d_flat,
+                           counts, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps);
       else
         klaunch(c, k_frame<T, RNG, MAXM, PRUNE, SP>, dim3(a.nblk), dim3(kBlock), lds, a, table,
                            prior, post, w0, w1, c->d_part[0], c->d_part[1], c->d_bscan[0], c->d_bscan[1],
-                           c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl, c->d_cpart, c->d_cgroup, gcount_w,
+                           c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_ctrl,
+                           tree_count ? c->d_cpart : gran_count(c), c->d_cgroup, gcount_w,
                            tcount_w, gcount_r, tcount_r, c->d_gen, counts, c->d_cand, c->d_mlpose, c->d_out, seq,
-                           c->d_stamps, (c->diag & kDiagTreeCount) ? nullptr : c->d_flat);
+                           c->d_stamps, tree_count ? nullptr : c->d_flat);
     }));
     *launched = true;
     if (wait_frame(c) != PFMPE_OK) {
@@ -730,8 +757,10 @@ struct Seq {
     const size_t need = BlobTable<T>::lds_bytes(fa_in.tbytes);
     uint32_t* counts = c->record_counts ? c->d_counts : nullptr;
     if (c->srv_alive && (c->srv_fn != fn || c->srv_nblk != fa_in.nblk || c->srv_lds < need || c->srv_counts != counts ||
-                         c->srv_j >= kSrvSlots || now_ns() - c->srv_last_ns > kSrvIdleNs))
+                         c->srv_j >= kSrvSlots || now_ns() - c->srv_last_ns > kSrvIdleNs || c->gframe >= kGranFrames))
       RET(srv_stop(c));
+    uint32_t gtag = 0;
+    RET(next_gtag(c, &gtag));  // zeroing on wrap goes before a launch: the server was stopped above if it ran
     if (!c->srv_alive) {
       // LDS with a margin over this frame's table (the tables of later frames vary), if the grid still fits at
       // two blocks per CU (frame_fused's residency rule); else exactly this table's
@@ -798,16 +827,17 @@ struct Seq {
     FrameArgsT<T> a = fa_in;
     a.flat_base_w = c->flat_base_w;
     a.flat_base_c = c->flat_base_c;
+    a.gtag = gtag;
     c->seq = (c->seq + 1) & 0x3fffffff;
     std::memcpy((void*)&m->fa, (const void*)&a, sizeof(a));
     m->prior = (const SP*)c->d_state[c->prior_idx];
     m->post = (SP*)c->d_state[1 - c->prior_idx];
     m->w0 = (T*)c->d_w[0];
     m->w1 = (T*)c->d_w[1];
-    m->part0 = c->d_part[0];
-    m->part1 = c->d_part[1];
+    m->part0 = gran_part(c, 0);
+    m->part1 = gran_part(c, 1);
     m->ctrl = c->d_ctrl;
-    m->cpart = c->d_cpart;
+    m->cpart = gran_count(c);
     m->flat = c->d_flat;
     m->counts = counts;
     m->cand = c->d_cand;
@@ -828,6 +858,7 @@ struct Seq {
     }
     c->srv_timed[c->srv_j] = c->timing_now ? 1 : 0;
     c->srv_j += 1;
+    const int64_t t_ring = now_ns();
     __atomic_store_n((uint64_t*)c->h_srv, (uint64_t)c->srv_j, __ATOMIC_SEQ_CST);
     *served = true;
     // the record, bounded by the frame's own waits (weighing and count barriers) plus the idle margin
@@ -839,6 +870,12 @@ struct Seq {
       return PFMPE_OK;
     }
     c->srv_last_ns = now_ns();
+    if (c->srv_j > 1 && c->srv_rec_ns) {  // consecutive frames of one dispatch
+      c->srv_host_ns += t_ring - c->srv_rec_ns;
+      c->srv_wait_ns += c->srv_last_ns - t_ring;
+      c->srv_timed_frames += 1;
+    }
+    c->srv_rec_ns = c->srv_last_ns;
     c->srv_frames += 1;
     const OutDev& o = *(const OutDev*)c->h_out;
     c->flat_base_w += (uint32_t)o.iters * (uint32_t)a.nblk;

@@ -89,7 +89,7 @@ size_t build_table(const pfmpe_ctx* c, const double* blobs, int B, unsigned char
 void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart, c->d_winkey,
-                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
+                 c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_gran, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
                  c->d_stamps, c->d_owner[0], c->d_owner[1], c->d_srv, c->d_srv_seq};
   for (void* p : dev)
     if (p) (void)hipFree(p);
@@ -244,6 +244,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_cand, (size_t)c->max_blk * sizeof(Cand)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_mlpose, 12 * sizeof(double)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_flat, kFlatWords * sizeof(uint32_t)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_gran, kGranBytes) == hipSuccess;
   {
     int coop = 0;
     ok = ok && hipDeviceGetAttribute(&c->num_cu, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess;
@@ -267,6 +268,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok = ok && hipMemsetAsync(c->d_cand, 0, (size_t)c->max_blk * sizeof(Cand), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_gran, 0, kGranBytes, c->stream) == hipSuccess;  // no stale word holds a live tag
   ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[0], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[1], 0, state_bytes, c->stream) == hipSuccess;
@@ -802,6 +804,9 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
     case PFMPE_INFO_SERVER_DISPATCHES: *value = c->srv_dispatches; return PFMPE_OK;
     case PFMPE_INFO_SERVER_FRAMES: *value = c->srv_frames; return PFMPE_OK;
+    case 100: *value = c->srv_host_ns; return PFMPE_OK;  // undocumented: resident host timing (diagnostics)
+    case 101: *value = c->srv_wait_ns; return PFMPE_OK;
+    case 102: *value = c->srv_timed_frames; return PFMPE_OK;
     default: return PFMPE_E_ARG;
   }
 }

@@ -31,8 +31,23 @@ for resident in (1, 0):
     for f in frames[5:]:
         eng.step(f)
     el = (time.perf_counter() - t0) / (len(frames) - 5)
+    hn, wn, fn = eng.info(100), eng.info(101), eng.info(102)
     n, ms = eng.kernel_stats()["k_frame"]
     print(f"resident={resident}: {el * 1e6:.2f} us/frame host, device {ms * 1e3 / max(n, 1):.2f} us/frame ({n} timed)")
+    if fn:
+        print(f"    host record -> next doorbell {hn / fn / 1e3:.2f} us, doorbell -> record {wn / fn / 1e3:.2f} us ({fn})")
+    # the C loop (pfmpe_step_batch), timing off
+    prepared = eng.prepare_batch(frames[5:])
+    eng.run_batch(prepared)
+    h0, w0, f0 = eng.info(100), eng.info(101), eng.info(102)
+    t0 = time.perf_counter()
+    eng.run_batch(prepared)
+    el = (time.perf_counter() - t0) / (len(frames) - 5)
+    fn = eng.info(102) - f0
+    msg = f"    C loop {el * 1e6:.2f} us/frame"
+    if fn:
+        msg += f"; host record -> next doorbell {(eng.info(100) - h0) / fn / 1e3:.2f} us, doorbell -> record {(eng.info(101) - w0) / fn / 1e3:.2f} us"
+    print(msg)
     eng.set_option(pf.OPT_TIMING, 0)
     eng.set_option(99, 4)
     for f in frames[:3]:
