@@ -2947,6 +2947,7 @@ struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B wor
 // round skips the stream (batch_block / k_resample_final_multi test status[s] == gen), so no pointer of a bad
 // descriptor is ever followed.  The host finds the missing frame record and reports the descriptor the device
 // saw (its HBM copy, written here word for word) against the one it wrote.
+constexpr uint32_t kMapKept = 0xffffffffu;  // k_stage_multi's boff: the block map is unchanged
 template <typename T, typename SP>
 __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __restrict__ host,
                                                         unsigned char* __restrict__ dev, uint32_t doff, uint32_t tbytes,
@@ -2990,8 +2991,10 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
   const unsigned char* tab = ld.table;
   // the map entries [first, first + nblk): 16-B stores of eight entries where a whole aligned group of eight is the
   // stream's (a C4 stream's 39k entries were 153 two-byte stores per thread: 10 us of staging), single entries at
-  // the two ends.  boff is 16-B aligned (batch_layout).
-  uint16_t* bm = (uint16_t*)(dev + boff);
+  // the two ends.  boff is 16-B aligned (batch_layout); kMapKept: the map in HBM is already this batch's (the host
+  // keeps the layout of the last batch it staged: the same streams, sizes and offsets), nothing to write
+  uint16_t* bm = (uint16_t*)(dev + (boff == kMapKept ? 0u : boff));
+  if (boff != kMapKept) {
   const int g0 = (first + 7) >> 3, g1 = (first + nblk) >> 3;  // whole groups of eight: [g0, g1)
   if (g1 > g0) {
     const uint32_t v = (uint32_t)s | ((uint32_t)s << 16);
@@ -3001,6 +3004,7 @@ __global__ __launch_bounds__(kBlock) void k_stage_multi(const unsigned char* __r
     for (int b = 8 * g1 + (int)threadIdx.x; b < first + nblk; b += kBlock) bm[b] = (uint16_t)s;
   } else {
     for (int b = threadIdx.x; b < nblk; b += kBlock) bm[first + b] = (uint16_t)s;
+  }
   }
   const uintptr_t to = (uintptr_t)tab - (uintptr_t)dev;  // wraps above tbytes for bank tables
   if (to < tbytes) {

@@ -61,7 +61,10 @@ __device__ __forceinline__ uint32_t mulhi_u(uint32_t a, uint32_t b) { return (ui
 __device__ __forceinline__ Phx2 philox_motion_pair(uint32_t nA, uint32_t nB, uint32_t c1, uint32_t c2, uint32_t c3,
                                                    uint32_t k0, uint32_t k1) {
   constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
-  // c1, c2, c3, k0, k1: kernel arguments (SGPRs), so the uniform products and xors below are scalar
+  // c1, c2, c3, k0, k1: kernel arguments (SGPRs), so the uniform products and xors below are scalar.  They are
+  // loop-invariant in the task loop; pinned per call, the ~12 scalar ops run per task instead of their results
+  // being hoisted into SGPRs that spilled to VGPR lanes (a v_readlane, a VALU slot, per use)
+  asm volatile("" : "+s"(c1), "+s"(c2), "+s"(c3), "+s"(k0), "+s"(k1));
   // round 1: p1 = M1 * c2 (uniform): n0 = hi(p1) ^ c1 ^ k0, n1 = lo(p1) uniform; p0 = M0 * n (per lane)
   const uint32_t r1n0 = mulhi_u(M1, c2) ^ c1 ^ k0;
   const uint32_t r1n1 = M1 * c2;

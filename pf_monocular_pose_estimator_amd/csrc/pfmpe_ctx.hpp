@@ -39,10 +39,15 @@ struct EventPair {
   int kid;
 };
 
-// An event recorded on a batch leader's stream after each batch it ran (pfmpe_step_multi).  Shared by the
-// batch's other contexts until their next work is ordered after it; destroyed with the last reference.
+// A batch leader's fence (pfmpe_step_multi), shared by the batch's other contexts until their next work is ordered
+// after the batch; destroyed with the last reference.  The event is recorded on the leader's stream lazily, when a
+// member needs the order (order_after, destroy): a record then captures the batch as well as one right after it
+// would, and a steady multi-stream loop, whose members never use their own streams, records nothing (one record
+// per batch cost 3-5 us of host time per batch).  stream: the leader's stream; null once the leader was destroyed
+// (its destroy drained the stream first, so nothing of the batch is pending then).
 struct BatchFence {
   hipEvent_t ev = nullptr;
+  hipStream_t stream = nullptr;
   ~BatchFence() {
     if (ev) (void)hipEventDestroy(ev);
   }
@@ -131,6 +136,9 @@ struct pfmpe_ctx {
   // host-side timing of served frames (undocumented info keys 100-102): record -> next doorbell (host work between
   // frames), doorbell -> record (the frame as the host sees it), frames counted
   int64_t srv_host_ns = 0, srv_wait_ns = 0, srv_timed_frames = 0, srv_rec_ns = 0;
+  // host-side timing of batches this context leads (undocumented info keys 110-114): entry -> first launch,
+  // the launches, last launch -> records, records -> return, batches counted
+  int64_t mt_enter = 0, mt_ns[4] = {0, 0, 0, 0}, mt_batches = 0;
   bool tbl_pending = false;        // h_table holds this frame's table, not yet copied to d_table (resident mode)
   size_t tbl_bytes = 0;
   Ctrl* d_ctrl = nullptr;
@@ -161,6 +169,7 @@ struct pfmpe_ctx {
   unsigned char* hd_multi = nullptr;  // device address of h_multi
   size_t multi_cap = 0;
   uint32_t multi_gen = 0;  // batch generation: one per staging launch this context leads (StreamDesc::gen)
+  std::vector<int64_t> map_sig;  // the block map now in d_multi: {boff, total, then (first, nblk) per stream}
   // Cross-stream ordering.  A context's work runs on its own stream (pfmpe_step, read-backs, ...) or, inside a
   // batch, on the batch leader's stream.  last_stream is where its latest work went (nullptr: none since
   // create); when the next work goes to a different stream it is ordered after that work: through the
@@ -236,7 +245,10 @@ inline int fail(pfmpe_ctx* c, int code, const std::string& msg) {
 inline int order_after(pfmpe_ctx* c, hipStream_t to, pfmpe_ctx* err) {
   if (!c->last_stream || c->last_stream == to) return PFMPE_OK;
   if (c->last_fence) {
-    HIPCHK(err, hipStreamWaitEvent(to, c->last_fence->ev, 0));
+    if (c->last_fence->stream) {
+      HIPCHK(err, hipEventRecord(c->last_fence->ev, c->last_fence->stream));
+      HIPCHK(err, hipStreamWaitEvent(to, c->last_fence->ev, 0));
+    }
   } else {
     if (!c->own_ev) HIPCHK(err, hipEventCreateWithFlags(&c->own_ev, hipEventDisableTiming));
     HIPCHK(err, hipEventRecord(c->own_ev, c->last_stream));
@@ -1110,9 +1122,23 @@ struct Seq {
       // stream (k_stage_multi reads the pinned image once), not by a copy-engine transfer
       const Desc* dd = (const Desc*)(d + Lt.doff);
       const uint16_t* db = (const uint16_t*)(d + Lt.boff);
+      // the block map is rewritten only when this batch's layout differs from the one staged last (a steady
+      // multi-stream loop stages it once: 2 x C4's 78k entries were most of k_stage_multi's 8 us)
+      std::vector<int64_t> sig;
+      sig.reserve(2 + 2 * (size_t)na);
+      sig.push_back((int64_t)Lt.boff);
+      sig.push_back(total);
+      for (int i = 0; i < na; ++i) {
+        sig.push_back(want[i].first_blk);
+        sig.push_back(want[i].fa.nblk);
+      }
+      const bool map_kept = sig == c0->map_sig;
+      c0->map_sig.swap(sig);
+      const int64_t t_l0 = now_ns();
+      if (round == 0) c0->mt_ns[0] += t_l0 - c0->mt_enter;
       RET(launch_ext(c0, PFMPE_K_AUX, [&] {
         klaunch(c0, k_stage_multi<T, SP>, dim3((unsigned)na), dim3(kBlock), 0, hdev, d, (uint32_t)Lt.doff,
-                (uint32_t)(round == 0 ? tbytes : 0), (uint32_t)Lt.boff, dstat, gen);
+                (uint32_t)(round == 0 ? tbytes : 0), map_kept ? kMapKept : (uint32_t)Lt.boff, dstat, gen);
       }));
       for (int k = 0; k < nit; ++k, ++iter) {
         if constexpr (kPkInstance<T, RNG, MAXM, SP>) {
@@ -1167,6 +1193,8 @@ struct Seq {
         klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd,
                 (const uint32_t*)dstat, gen);
       }));
+      const int64_t t_l1 = now_ns();
+      c0->mt_ns[1] += t_l1 - t_l0;
       std::vector<int> next;
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
@@ -1174,6 +1202,7 @@ struct Seq {
           return batch_failure(c0, cs, act, want, d + Lt.doff, dstat, gen, c->err);
         if (!frame_done(c)) next.push_back(act[i]);
       }
+      c0->mt_ns[2] += now_ns() - t_l1;
       if (next.empty()) break;
       for (int s : next) {
         const FrameArgsT<T>& fa = fas[s];
@@ -1317,6 +1346,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     c0->h_multi = nullptr;
     c0->hd_multi = nullptr;
     c0->multi_cap = 0;
+    c0->map_sig.clear();  // a new scratch holds no map
     const size_t cap = std::max(need * 2, (size_t)1 << 16);
     HIPCHK(c0, hipMalloc((void**)&c0->d_multi, cap));
     // read by k_stage_multi over PCIe: mapped, coherent (the host rewrites it between batches)
@@ -1329,6 +1359,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   if (!c0->lead_fence) {  // created before any member's ordering state changes (no early return after)
     auto f = std::make_shared<BatchFence>();
     HIPCHK(c0, hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
+    f->stream = c0->stream;
     c0->lead_fence = f;
   }
   // every member's work so far is ordered before the batch (its own stream, or an earlier batch led elsewhere).
@@ -1367,15 +1398,12 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
   else
     rc = Seq<T, RNG, 16, SP>::step_multi(cs, S, fas.data(), tables.data(), c0->h_multi, c0->hd_multi, c0->d_multi, tbytes);
   // the batch's kernels may still be retiring when the records are in (or when a step failed part-way): each
-  // member's next work on its own stream waits for the fence (the leader's own stream is the batch stream).
-  // Set whatever step_multi returned; without a recorded fence a member orders after the batch stream itself
-  // (order_after records its own event there)
-  const bool fenced = hipEventRecord(c0->lead_fence->ev, c0->stream) == hipSuccess;
+  // member's next work on its own stream is ordered after the leader's stream through the fence, recorded when
+  // that work comes (the leader's own stream is the batch stream).  Set whatever step_multi returned.
   for (int s = 0; s < S; ++s) {
     cs[s]->last_stream = c0->stream;
-    cs[s]->last_fence = (s == 0 || !fenced) ? nullptr : c0->lead_fence;
+    cs[s]->last_fence = s == 0 ? nullptr : c0->lead_fence;
   }
-  if (!fenced && rc == PFMPE_OK) return fail(c0, PFMPE_E_HIP, "step_multi: recording the batch fence failed");
   return rc;
 }
 

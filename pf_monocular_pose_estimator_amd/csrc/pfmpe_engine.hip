@@ -283,8 +283,14 @@ void pfmpe_destroy(pfmpe_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)srv_stop(c);  // the resident server's exit message, else the stream drains only at its idle bound
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->last_fence) (void)hipEventSynchronize(c->last_fence->ev);  // a batch led by another context
+  if (c->last_fence && c->last_fence->stream) {  // a batch led by another context: its stream up to now
+    if (hipEventRecord(c->last_fence->ev, c->last_fence->stream) == hipSuccess)
+      (void)hipEventSynchronize(c->last_fence->ev);
+    else
+      (void)hipStreamSynchronize(c->last_fence->stream);
+  }
   c->last_fence.reset();
+  if (c->lead_fence) c->lead_fence->stream = nullptr;  // drained above; members find nothing pending
   c->lead_fence.reset();
   if (c->own_ev) (void)hipEventDestroy(c->own_ev);
   free_all(c);
@@ -534,6 +540,7 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
     const int rc = check_step(c, &in[s], &out[s]);
     if (rc != PFMPE_OK) return fail(c0, rc, who + c->err);  // the per-stream code (E_ARG / E_CAP / E_STATE)
   }
+  c0->mt_enter = now_ns();
   RET(set_device(c0));
   c0->timing_now = c0->timing > 0 && (c0->timing_frame++ % c0->timing) == 0;  // batches timed on the leader
   const bool ref = c0->params.rng_mode == PFMPE_RNG_REFERENCE;
@@ -553,10 +560,13 @@ int pfmpe_step_multi(pfmpe_ctx* const* ctxs, int S, const pfmpe_frame_in* in, pf
   if (rs != PFMPE_OK) c0->ev_used = ev_mark;  // only the failed batch's own brackets are dropped
   else if (c0->ev_used >= kHarvestPairs) RET(harvest_timing(c0));
   RET(rs);
+  const int64_t t_r = now_ns();
   for (int s = 0; s < S; ++s) {
     take_step(ctxs[s], &in[s], &out[s]);
     if (!ctxs[s]->fused) ctxs[s]->clean_since_fallback += 1;  // a clean two-launch frame (PFMPE_OPT_FUSED_REARM)
   }
+  c0->mt_ns[3] += now_ns() - t_r;
+  c0->mt_batches += 1;
   return PFMPE_OK;
 }
 
@@ -807,6 +817,8 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case 100: *value = c->srv_host_ns; return PFMPE_OK;  // undocumented: resident host timing (diagnostics)
     case 101: *value = c->srv_wait_ns; return PFMPE_OK;
     case 102: *value = c->srv_timed_frames; return PFMPE_OK;
+    case 110: case 111: case 112: case 113: *value = c->mt_ns[key - 110]; return PFMPE_OK;  // batch host timing
+    case 114: *value = c->mt_batches; return PFMPE_OK;
     default: return PFMPE_E_ARG;
   }
 }
