@@ -1948,6 +1948,30 @@ __device__ __forceinline__ void copy_table(const unsigned char* __restrict__ src
   for (int i = threadIdx.x; i < n4; i += kBlock) d4[i] = s4[i];
 }
 
+// copy_table + stage_consts_from with every load issued before the first LDS store: one memory round trip for the
+// table (its first 8 KB: two 16-B loads per thread), the frame constants and whatever the caller issued before
+// (k_frame2: the prior), instead of one per loop and per copy
+template <typename T>
+__device__ __forceinline__ void stage_table_consts(const unsigned char* __restrict__ src, unsigned char* dst, size_t bytes,
+                                                   const uint32_t* cw_src, LdsConst<T>& sc) {
+  typedef __attribute__((address_space(1))) const u32x4_t gv4_t;
+  gv4_t* s4 = (gv4_t*)src;
+  u32x4_t* d4 = (u32x4_t*)dst;
+  const int n4 = (int)(bytes / 16);
+  const int t = threadIdx.x;
+  constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
+  static_assert(kWordsC <= kBlock, "one constant word per thread");
+  u32x4_t r0 = {0u, 0u, 0u, 0u}, r1 = {0u, 0u, 0u, 0u};
+  uint32_t cw = 0u;
+  if (t < n4) r0 = s4[t];
+  if (t + kBlock < n4) r1 = s4[t + kBlock];
+  if (t < kWordsC) cw = cw_src[t];
+  if (t < n4) d4[t] = r0;
+  if (t + kBlock < n4) d4[t + kBlock] = r1;
+  if (t < kWordsC) ((uint32_t*)&sc)[t] = cw;
+  for (int i = t + 2 * kBlock; i < n4; i += kBlock) d4[i] = s4[i];  // tables past 8 KB (large B)
+}
+
 // Control record / scan records move between blocks of one launch (and, in k_frame, between the
 // iterations of one launch) through write-through words only.
 __device__ __forceinline__ Ctrl load_ctrl_wt(const Ctrl* __restrict__ ctrl) {
@@ -4532,10 +4556,11 @@ __device__ __forceinline__ bool frame2_body(
   const int lane = lane_id(), wv = wave_id();
   const int blk = blockIdx.x, g_own = blk / fa.gsz;
 
-  copy_table(table, smem, (size_t)fa.tbytes);
+  // the prior's loads first: in flight together with the table's, one memory round trip before the weighing
+  // instead of two (the table's wait would otherwise come before the prior loads were even issued)
   T A[12];
   if (valid && n >= 2) load_prior<T, SP, WT ? kPolSc1 : 0>(fa, prior, n, A);
-  stage_consts_from(fa_words, sc);
+  stage_table_consts(table, smem, (size_t)fa.tbytes, fa_words, sc);
   if (threadIdx.x == 0) {
     fl.c = zero_ctrl();  // start of frame: every block keeps an identical copy of the control record
     fl.abort = 0;
