@@ -1648,6 +1648,7 @@ enum : int {
   kDiagCorruptDesc = 8192, // pfmpe_step_multi: the first stream's descriptor is altered after its tag (test of the
                            // staging check; the altered word is a key word, never a pointer)
   kDiagNoDefer = 16384,    // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
+  kDiagMinSide = 65536,      // k_frame2: run the zmin scans (group_zmin2) even when no weight can be negative (tests)
   kDiagBlockResample = 32768  // deferred two-launch frames resample with the block-per-256 k_resample instead of
                               // k_resample_owners' wave per 256 (A/B, identity tests)
 };
@@ -4360,6 +4361,7 @@ struct Frame2Lds {
   GroupPart gp[2][kFlatMaxGroups];  // group partials per weight slot (sum, zmax, zmin; latest iteration)
   WaveArg wa[2][kWaves];            // per weight slot: each wave's max / argmax, min / argmin over its blocks
   BlockScan bs[2];                  // this block's in-group scan words per slot
+  int dirty[kWaves];                // group_math2: a wave's blocks may hold a negative or NaN weight
   GroupScan gs;                     // this block's group prefix / running max (kept slot)
   Ctrl c;
   int abort;
@@ -4374,10 +4376,23 @@ struct BlockIn {
   bool vb, mine;
   BlockPart p;
 };
-__device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&out)[2], BlockScan* own, WaveArg& wa) {
+// The min side (min / argmin, and the zmin running-min scans) only matters when the kept iteration's S < 0, i.e.
+// with a negative weight, and the NaN test below (S = NaN reaches the zin_min select of the resampling).  Two
+// shortcuts, each exact:
+//  - argmin chain: an fp32 wave with no negative weight leaves its min side as the pair (+inf, 0x7fffffff)
+//    (wave_weight_partials), and so does every block built from such waves; when every block of this wave holds
+//    that pair, the chain's result is that pair, so it is not run (wave-uniform test);
+//  - zmin scans: left to group_zmin2, which frame2_body runs only when some block of the iteration (any wave: the
+//    test is made block-wide after the next barrier) holds a negative minimum or a NaN sum.  Otherwise every weight
+//    is >= 0 and none is NaN, so S >= 0, and no consumer reads zmin / zin_min (top_math_regs' cm takes zmax when
+//    S > 0 and skips S == 0; a frame with S == 0 is not accepted, so it is not resampled).
+// group_math2 returns whether this wave's blocks fail that test, and leaves the zmin scans' inputs in zmin_in.
+__device__ __forceinline__ bool group_math2(const BlockIn (&in)[2], GroupPart (&out)[2], BlockScan* own, WaveArg& wa,
+                                            double (&zmin_in)[2]) {
   double sum[2], maxrel[2], minrel[2];
   double maxw = -INFINITY, minw = INFINITY;
   int amax = 0x7fffffff, amin = 0x7fffffff;
+  bool min_placeholder = true, dirty = false;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const bool vb = in[k].vb;
@@ -4385,57 +4400,87 @@ __device__ __forceinline__ void group_math2(const BlockIn (&in)[2], GroupPart (&
       cmb_max(maxw, amax, in[k].p.maxw, in[k].p.argmax);
       cmb_min(minw, amin, in[k].p.minw, in[k].p.argmin);
     }
+    min_placeholder &= !vb || (in[k].p.minw == (double)INFINITY && in[k].p.argmin == 0x7fffffff);
+    dirty |= vb && !(in[k].p.minw >= 0.0 && in[k].p.sum == in[k].p.sum);
     sum[k] = vb ? in[k].p.sum : 0.0;
     maxrel[k] = vb ? in[k].p.maxrel : -INFINITY;
     minrel[k] = vb ? in[k].p.minrel : INFINITY;
   }
   double incl[2] = {sum[0], sum[1]};
-  scan_steps([&](auto st) {
-    using S = decltype(st);
-    st_sum<S>(incl[0]);
-    st_sum<S>(incl[1]);
-    st_argmax<S>(maxw, amax);
-    st_argmin<S>(minw, amin);
-  });
-  double E[2], zi_max[2], zi_min[2];
+  if (__builtin_amdgcn_ballot_w64(!min_placeholder) == 0) {
+    scan_steps([&](auto st) {
+      using S = decltype(st);
+      st_sum<S>(incl[0]);
+      st_sum<S>(incl[1]);
+      st_argmax<S>(maxw, amax);
+    });
+    minw = INFINITY;  // the argmin chain over inputs that are all this pair
+    amin = 0x7fffffff;
+  } else {
+    scan_steps([&](auto st) {
+      using S = decltype(st);
+      st_sum<S>(incl[0]);
+      st_sum<S>(incl[1]);
+      st_argmax<S>(maxw, amax);
+      st_argmin<S>(minw, amin);
+    });
+    bcast63(minw, amin);
+  }
+  double E[2], zi_max[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     E[k] = 0.0 + wave_shr1(incl[k], 0.0);
     zi_max[k] = in[k].vb ? E[k] + maxrel[k] : -INFINITY;
-    zi_min[k] = in[k].vb ? E[k] + minrel[k] : INFINITY;
+    zmin_in[k] = in[k].vb ? E[k] + minrel[k] : INFINITY;
   }
   scan_steps([&](auto st) {
     using S = decltype(st);
     st_max<S>(zi_max[0]);
     st_max<S>(zi_max[1]);
-    st_min<S>(zi_min[0]);
-    st_min<S>(zi_min[1]);
   });
   bcast63(maxw, amax);
-  bcast63(minw, amin);
   wa.maxw = maxw;
   wa.minw = minw;
   wa.argmax = amax;
   wa.argmin = amin;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
-    double zp_max = wave_shr1(zi_max[k], -(double)INFINITY), zp_min = wave_shr1(zi_min[k], (double)INFINITY);
+    double zp_max = wave_shr1(zi_max[k], -(double)INFINITY);
     zp_max = zp_max > -INFINITY ? zp_max : -INFINITY;
-    zp_min = zp_min < INFINITY ? zp_min : INFINITY;
     if (in[k].vb && in[k].mine) {
       own->E = E[k];
       own->zin_max = zp_max;
-      own->zin_min = zp_min;
+      own->zin_min = INFINITY;  // group_zmin2, when needed
       own->pad = 0.0;
     }
-    const double tmax = lane_value(zi_max[k], 63), tmin = lane_value(zi_min[k], 63);
+    const double tmax = lane_value(zi_max[k], 63);
     GroupPart& r = out[k];
     r.sum = 0.0 + lane_value(incl[k], 63);
     r.zmax = tmax > -INFINITY ? tmax : -INFINITY;
-    r.zmin = tmin < INFINITY ? tmin : INFINITY;
+    r.zmin = INFINITY;   // group_zmin2, when needed
     r.maxw = -INFINITY;  // unused on this path (wa)
     r.minw = INFINITY;
     r.argmax = r.argmin = 0x7fffffff;
+  }
+  return __builtin_amdgcn_ballot_w64(dirty) != 0;
+}
+// the zmin running-min scans of group_math2's two groups (propagate_group's arithmetic): the block's own zin_min and
+// the groups' zmin, into the LDS words group_math2 left as placeholders
+__device__ __forceinline__ void group_zmin2(const BlockIn (&in)[2], double (&zi_min)[2], BlockScan* own, GroupPart* gp0,
+                                            GroupPart* gp1) {
+  scan_steps([&](auto st) {
+    using S = decltype(st);
+    st_min<S>(zi_min[0]);
+    st_min<S>(zi_min[1]);
+  });
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    double zp_min = wave_shr1(zi_min[k], (double)INFINITY);
+    zp_min = zp_min < INFINITY ? zp_min : INFINITY;
+    if (in[k].vb && in[k].mine) own->zin_min = zp_min;
+    const double tmin = lane_value(zi_min[k], 63);
+    GroupPart* g = k ? gp1 : gp0;
+    if (g && lane_id() == 0) g->zmin = tmin < INFINITY ? tmin : INFINITY;
   }
 }
 
@@ -4643,6 +4688,8 @@ __device__ __forceinline__ bool frame2_body(
     // every block: the group partials from all block partials, then the top.  Groups are 64 blocks, so
     // thread t owns blocks t and t + 256 and wave w reduces groups w and w + 4; all six 16-B loads of the
     // thread are in flight together (one round trip)
+    BlockIn in[2];
+    double zmin_in[2];
     {
       const BlockPart* pp = (iter & 1) ? part1 : part0;  // iteration parity (see the store above)
       if ((fa.diag & kDiagLagLoads) && blk == fa.nblk - 1) {  // a lagging reader (the race test)
@@ -4656,7 +4703,6 @@ __device__ __forceinline__ bool frame2_body(
       ld_part_issue(pp + (v1 ? b1 : 0), r1);
       wait_parts(r0, r1);
       if (stamps && threadIdx.x == 0) stamp_max(stamps, 24, rt_now());
-      BlockIn in[2];
       in[0].vb = v0;
       in[0].mine = b0 == blk;
       in[0].p = unpack_part(r0);
@@ -4665,13 +4711,24 @@ __device__ __forceinline__ bool frame2_body(
       in[1].p = unpack_part(r1);
       GroupPart gp[2];
       WaveArg wa;
-      group_math2(in, gp, &fl.bs[slot], wa);
+      const bool dirty = group_math2(in, gp, &fl.bs[slot], wa, zmin_in);
       if (lane == 0) fl.wa[slot][wv] = wa;
       if (lane == 0 && wv < fa.ngrp) fl.gp[slot][wv] = gp[0];
       if (lane == 0 && wv + kWaves < fa.ngrp) fl.gp[slot][wv + kWaves] = gp[1];
+      if (lane == 0) fl.dirty[wv] = dirty;
     }
     if (stamps && threadIdx.x == 0) stamp_max(stamps, 25, rt_now());
     __syncthreads();
+    // the zmin scans only when some block of the iteration may hold a negative or NaN weight (group_math2's note);
+    // every block reads the same partials, so every block takes the same branch
+    int dirty = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) dirty |= fl.dirty[w];
+    if (dirty || (fa.diag & kDiagMinSide)) {
+      group_zmin2(in, zmin_in, &fl.bs[slot], wv < fa.ngrp ? &fl.gp[slot][wv] : nullptr,
+                  wv + kWaves < fa.ngrp ? &fl.gp[slot][wv + kWaves] : nullptr);
+      __syncthreads();
+    }
     if (wv == 0) {
       // field-wise LDS reads (an aggregate copy of the conditional struct went through scratch)
       auto qk = [&](int ks) {
