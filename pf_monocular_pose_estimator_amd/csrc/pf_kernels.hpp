@@ -3135,6 +3135,45 @@ __device__ __forceinline__ int pairs_from_minima(const FrameArgsT<T>& fa, const 
   wave_lds_sync();
   return np;
 }
+// pose_pairs' per-marker wave arg-minimum in fp32: wave_argmin's lexicographic (distance, original index) minimum,
+// as two integer minimum reductions per marker.  Every lane's best is a number (it starts at +inf and a NaN distance
+// never replaces it) and >= +0 (a sum of squares), so its bits order as integers and equal distances have equal bits:
+// the minimum's bits first, then the lowest index among the lanes holding them.  One DPP-fed v_min_i32 per step (the
+// quad / half-row / row / bcast pattern of wave_total_lane63: lane 63 ends with the whole wave; the bcast steps leave
+// rows no one reads), all MAXM markers interleaved, instead of the (value, index) select chains.
+template <int MAXM>
+__device__ __forceinline__ void wave_argmin_dist(float (&best)[MAXM], int (&arg)[MAXM]) {
+  auto wave_min_lane63 = [](int (&k)[MAXM]) {
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppQuadXor1, 0xf, 0xf, false));
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppQuadXor2, 0xf, 0xf, false));
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppRowHalfMirror, 0xf, 0xf, false));
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppRowMirror, 0xf, 0xf, false));
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppBcast15, 0xa, 0xf, false));
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) k[j] = min(k[j], __builtin_amdgcn_mov_dpp(k[j], kDppBcast31, 0xc, 0xf, false));
+  };
+  int k[MAXM], c[MAXM];
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) k[j] = (int)__float_as_uint(best[j]);
+  wave_min_lane63(k);
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    k[j] = __builtin_amdgcn_readlane(k[j], 63);
+    c[j] = (int)__float_as_uint(best[j]) == k[j] ? arg[j] : 0x7fffffff;
+  }
+  wave_min_lane63(c);
+#pragma unroll
+  for (int j = 0; j < MAXM; ++j) {
+    best[j] = __uint_as_float((uint32_t)k[j]);
+    arg[j] = __builtin_amdgcn_readlane(c[j], 63);
+  }
+}
+
 template <typename T, int MAXM>
 __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsConst<T>& sc, const LdsBlobs<T>& tb,
                                            const T* P, uint32_t* corr, int* np_out) {
@@ -3166,9 +3205,14 @@ __device__ __forceinline__ void pose_pairs(const FrameArgsT<T>& fa, const LdsCon
     }
   }
   // all MAXM reductions unconditionally (markers past M reduce +inf: harmless), so the DPP chains interleave
+  if constexpr (std::is_same<T, float>::value) {
+    wave_argmin_dist<MAXM>(best, arg);
+  } else {
+#pragma unroll
+    for (int j = 0; j < MAXM; ++j) wave_argmin(best[j], arg[j]);
+  }
 #pragma unroll
   for (int j = 0; j < MAXM; ++j) {
-    wave_argmin(best[j], arg[j]);
     m[j] = best[j];
     r[j] = arg[j] == 0x7fffffff ? 0 : arg[j];
   }

@@ -28,7 +28,7 @@ for N in [int(x) for x in sys.argv[1:]] or [100000]:
     names = {8: "K1 table built (last)", 19: "K1 table built (first)", 9: "K1 weights (last)", 10: "K2 scan (last)",
              11: "K2 counts (last)", 12: "K2 scatter (last)", 13: "fin Pm", 14: "fin P", 15: "fin minima",
              16: "fin score", 17: "fin record", 18: "fin published", 20: "K2 block argmax (last)",
-             21: "K2 rows staged (last)", 1: "K1 block partial (last)", 5: "K2 block partial (last)",
+             21: "K2 rows staged (last)", 22: "K2 candidate published (flat, last)", 1: "K1 block partial (last)", 5: "K2 block partial (last)",
              6: "K3 start", 24: "K3 winner reduced / flat partials loaded", 25: "K3 marker minima / flat groups", 26: "K3 pairs / flat top",
              27: "K1 propagated (wave 0, last)", 28: "K1 projected (wave 0, last)", 29: "K1 minima (wave 0, last)",
              2: "K1 barrier passed (flat, last)", 23: "K1 arrival issued (flat, last)", 31: "K1 barrier passed (flat, first)", 3: "K1 top done (flat, last)"}
