@@ -534,7 +534,7 @@ def main():
             plan += [(syn.CONFIGS["C5"], pf.STATE_F32, 48, 8, 2), (syn.CONFIGS["C5"], pf.STATE_F32, 48, 32, 2),
                      (syn.CONFIGS["C4"], pf.STATE_F16, 24, 2, 1)]
         for cfg_, st_, Sb_, S_, G_ in plan:
-            steps_ = args.multi_steps if cfg_.N <= 1_000_000 else max(10, args.multi_steps // 3)
+            steps_ = args.multi_steps if cfg_.N <= 1_000_000 else max(40, args.multi_steps)  # C4: ~20 ms timed
             pt = multi_stream_point(pf, syn, cfg_, S_, steps_, 5, st_, prm.rng_mode, device, sid, args.prune,
                                     args.keep_prop, G_, args.diag)
             pt["config"] = cfg_.name
