@@ -49,7 +49,10 @@ def parse():
     ap.add_argument("--state", default="", choices=["", "f32", "f16", "f64"],
                     help="particle state storage (default: f16 for C4 per BASELINE.json configs[3], else f32)")
     ap.add_argument("--cpu-frames", type=int, default=3, help="oracle frames for cpu_baseline (0 = skip)")
-    ap.add_argument("--no-timing", action="store_true", help="do not bracket kernels with HIP events")
+    ap.add_argument("--no-timing", action="store_true", help="no kernel pass (no HIP-event brackets at all)")
+    ap.add_argument("--kernel-frames", type=int, default=0,
+                    help="frames of the kernel pass after the timed region, every one HIP-event bracketed "
+                         "(0 = max(20, steps))")
     ap.add_argument("--timing-period", type=int, default=0,
                     help="HIP events bracket the kernels of every P-th timed frame; default: two frames up to 40 "
                          "timed frames, four beyond (a bracketed C2 frame costs ~12 us more, DESIGN.md §7)")
@@ -87,17 +90,28 @@ def parse():
     ap.add_argument("--single-steps", type=int, default=100, help="timed frames per --single-points config")
     ap.add_argument("--fused", type=int, default=2, choices=[0, 1, 2],
                     help="frame shape: 2 flat one-launch (default), 1 tree one-launch, 0 two launches")
-    ap.add_argument("--resident", type=int, default=0, choices=[0, 1],
-                    help="flat one-launch frames through the resident frame server (PFMPE_OPT_RESIDENT)")
     return ap.parse_args()
 
 
-def timing_period(steps: int) -> int:
-    """HIP-event sampling period: two bracketed frames up to 40 timed frames, four beyond.  A bracketed frame
-    (hipExtLaunchKernel with start / stop events) costs ~12 us more at C2, so the brackets are
-    kept few; their kernel averages agree with the rocprofv3 trace of the same command (profiles/r04/)."""
-    n = 2 if steps <= 40 else 4
-    return max(1, -(-steps // n))
+def info_or(pf, eng, key, default=-1):
+    """pfmpe_get_info, or `default` for a key an older library (an A/B build) does not know."""
+    try:
+        return eng.info(key)
+    except pf.PFError:
+        return default
+
+
+def kernel_pass(pf, eng, frames):
+    """Per-kernel average durations over `frames`, every frame's kernels HIP-event bracketed (hipExtLaunchKernel
+    dispatch timestamps, the same ones rocprofv3's kernel trace reads).  Run right after a timed region on the same
+    stream, so the timed frames carry no bracket (a bracketed frame costs the host ~12 us at C2) and
+    the averages cover every frame of the pass instead of a sample.  scripts/trace_check.py
+    takes the same launches out of a rocprofv3 trace of the same command."""
+    eng.reset_kernel_stats()
+    eng.set_option(pf.OPT_TIMING, 1)  # every frame
+    outs = eng.run_batch(eng.prepare_batch(frames))
+    eng.set_option(pf.OPT_TIMING, 0)
+    return eng.kernel_stats(), outs
 
 
 def algorithmic_bytes(S: int, N: int, k: float = 1.0) -> dict:
@@ -142,6 +156,22 @@ def pmc_traffic(path: str, kernel: str):
         return None
 
 
+def counter_bytes_per_update(path: str, N: int):
+    """HBM bytes per particle-update by counters: the frame's kernels' PMC bytes per launch (the committed one-stream
+    pass of the config, profiles/pmc_<cfg>_n<N>.json) over N.  The deferred design does not move the canonical 3S+8
+    bytes, so a batch point's canonical frac is not its DRAM occupancy."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            rows = json.load(f)
+    except (OSError, ValueError):
+        return None
+    frame = [k for k in rows if k.startswith("k_") and k not in ("k_import", "k_export", "k_regen", "k_weights_export")]
+    tot = sum(rows[k].get("hbm_bytes") or 0 for k in frame)
+    return tot / N if tot else None
+
+
 # The issue roofline (SURVEY.md §8d "report both fractions"): the kernels of this path have no MFMA work and at the
 # sizes that fit the MALL they are bound by instruction issue, not bytes.  From the committed PMC pass of the same
 # workload (scripts/pmc_lines.sh): VALU issue = SQ_INSTS_VALU (wave instructions) x the measured cost of one wave
@@ -161,7 +191,7 @@ def issue_roof(path: str, kernel: str, avg_us: float):
             rows = json.load(f)
     except (OSError, ValueError):
         return None
-    alias = {"k_frame": "k_frame2", "k_resample": "k_resample_owners"}
+    alias = {"k_frame": "k_frame2"}
     row = rows.get(kernel) or rows.get(alias.get(kernel, ""), None)
     if not row or "SQ_INSTS_VALU" not in row or "SQ_INSTS_SALU" not in row:
         return None
@@ -372,10 +402,12 @@ def multi_stream_point(pf, syn, base, S: int, steps: int, warmup: int, state_dty
 def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device: int, sid: int, args,
                         state_dtype=None, kernels=False):
     """One stream of `base` (f32 state unless given) on one GPU, timed as the main line is (pfmpe_step_batch:
-    every frame blocks on its record).  kernels: also bracket the kernels of a few timed frames with HIP
-    events (as the main line does) and report their averages, the frame shape and the weighing pass."""
+    every frame blocks on its record).  kernels: then a kernel pass of `kframes` more frames, every one HIP-event
+    bracketed (kernel_pass, as the main line), and their per-kernel averages, the frame shape and the weighing
+    pass."""
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=base.N, heavy=base.heavy, seed=sid)
-    st = syn.make_stream(cfg, warmup + steps)
+    kframes = max(20, steps) if kernels else 0
+    st = syn.make_stream(cfg, warmup + steps + kframes)
     eng = pf.Engine(device=device, max_particles=cfg.N,
                     state_dtype=pf.STATE_F32 if state_dtype is None else state_dtype)
     try:
@@ -393,10 +425,7 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
                                  dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index) for f in st.frames]
         for f in frames[:warmup]:
             eng.step(f)
-        if kernels:
-            eng.reset_kernel_stats()
-            eng.set_option(pf.OPT_TIMING, timing_period(steps))
-        prepared = eng.prepare_batch(frames[warmup:])
+        prepared = eng.prepare_batch(frames[warmup:warmup + steps])
         t0 = time.perf_counter()
         outs = eng.run_batch(prepared)
         el = time.perf_counter() - t0
@@ -404,14 +433,15 @@ def single_stream_point(pf, syn, base, steps: int, warmup: int, rng: int, device
               "ms_per_frame": el * 1e3 / steps, "frames": steps,
               "iters_per_frame": float(np.mean([o.iters for o in outs]))}
         if kernels:
-            eng.set_option(pf.OPT_TIMING, 0)
-            stats = eng.kernel_stats()
+            stats, _ = kernel_pass(pf, eng, frames[warmup + steps:])
+            pt["kernel_pass_frames"] = kframes
             pt["frame_shape"] = {0: "two-launch", 1: "k_frame", 2: "k_frame2"}.get(eng.info(pf.INFO_LAST_SHAPE))
             wname = {pf.WEIGH_STREAM: "k_weigh_stream", pf.WEIGH_PK: "k_weigh_pk"}.get(
                 eng.info(pf.INFO_LAST_WEIGH_PASS), "k_propagate_weigh")
             pt["weigh_pass"] = wname
-            pt["per_kernel_avg_us"] = {(wname if k == "k_propagate_weigh" else k): round(v[1] * 1e3 / v[0], 3)
-                                       for k, v in stats.items() if v[0] > 0}
+            rname = "k_resample_owners" if info_or(pf, eng, pf.INFO_LAST_RESAMPLE) == pf.RESAMPLE_OWNERS else "k_resample"
+            pt["per_kernel_avg_us"] = {{"k_propagate_weigh": wname, "k_resample": rname}.get(k, k):
+                                       round(v[1] * 1e3 / v[0], 3) for k, v in stats.items() if v[0] > 0}
             if pt["per_kernel_avg_us"]:
                 dom = max(pt["per_kernel_avg_us"], key=pt["per_kernel_avg_us"].get)
                 pmc = os.path.join(ROOT, "profiles", f"pmc_{cfg.name.lower()}_n{cfg.N}.json")
@@ -439,7 +469,8 @@ def main():
     sid = rank if args.stream_id < 0 else args.stream_id
     cfg = syn.StreamConfig(base.name, M=base.M, B=base.B, N=args.particles or base.N, heavy=base.heavy, seed=sid)
     n_frames = args.warmup + args.steps
-    st = syn.make_stream(cfg, n_frames)
+    kframes = 0 if args.no_timing else (args.kernel_frames or max(20, args.steps))
+    st = syn.make_stream(cfg, n_frames + kframes)
     state = args.state or ("f16" if cfg.name == "C4" else "f32")
     state_dtype = {"f32": pf.STATE_F32, "f16": pf.STATE_F16, "f64": pf.STATE_F64}[state]
     # one GPU per rank; PFMPE_BENCH_DEVICE pins every rank to one device (rehearsing the multi-rank launch
@@ -452,7 +483,6 @@ def main():
     eng.set_params(prm)
     eng.set_prior(st.prior())
     eng.set_option(pf.OPT_FUSED, args.fused)
-    eng.set_option(pf.OPT_RESIDENT, args.resident)
     eng.set_option(pf.OPT_PRUNE, args.prune)
     if args.keep_prop >= 0:
         eng.set_option(pf.OPT_KEEP_PROPAGATED, args.keep_prop)
@@ -463,13 +493,13 @@ def main():
                              dt=f.dt, seed=(sid << 32) + 17 + f.index, frame_idx=f.index,
                              force_iters=args.force_iters) for f in st.frames]
     if args.occlude:
-        frames = occluded_frames(eng, st, sid, n_frames, 0)
+        frames = occluded_frames(eng, st, sid, n_frames + kframes, 0)
 
     for i in range(args.warmup):
         eng.step(frames[i])
     eng.reset_kernel_stats()
-    if not args.no_timing:
-        eng.set_option(pf.OPT_TIMING, args.timing_period or timing_period(args.steps))
+    if args.timing_period > 0:  # diagnostics only: brackets inside the timed region
+        eng.set_option(pf.OPT_TIMING, args.timing_period)
 
     if dist:
         dist.barrier()
@@ -488,6 +518,10 @@ def main():
     accepted = sum(o.accepted for o in outs)
     stats = eng.kernel_stats()
     eng.set_option(pf.OPT_TIMING, 0)
+    kiters = iters
+    if kframes:  # the kernel pass: the stream's next kframes frames, every one bracketed (kernel_pass)
+        stats, kouts = kernel_pass(pf, eng, frames[n_frames:n_frames + kframes])
+        kiters = [o.iters for o in kouts]
     if args.dump_records:  # every timed frame's record + a digest of the final particle set, for the tests
         import hashlib
         post = eng.get_particles(1)
@@ -497,6 +531,7 @@ def main():
                        "post_sha1": hashlib.sha1(post.tobytes()).hexdigest()}, f)
     shape = eng.info(pf.INFO_LAST_SHAPE)
     weigh_pass = eng.info(pf.INFO_LAST_WEIGH_PASS)
+    resample_kind = info_or(pf, eng, pf.INFO_LAST_RESAMPLE)
     fallbacks = eng.info(pf.INFO_FUSED_FALLBACKS)
 
     elapsed, total_updates = combine_ranks(dist, elapsed, updates)
@@ -524,7 +559,9 @@ def main():
         Sb = {"f32": 48, "f16": 24, "f64": 96}[state]
         multi = {"what": "S independent streams of a config per GPU, one batch per frame (pfmpe_step_multi), "
                          "split into `groups` concurrent batches (one host thread and HIP stream each); "
-                         "frac = updates/s x (3S+8) B / 8 TB/s", "points": []}
+                         "frac = updates/s x (3S+8) B / 8 TB/s (canonical bytes); counter_frac = updates/s x the "
+                         "bytes per update the config's one-stream PMC pass measures / 8 TB/s (DRAM occupancy)",
+                 "points": []}
         gsweep = [int(x) for x in args.multi_groups.split(",") if x]
         plan = [(base, state_dtype, Sb, S_, G_) for S_ in [int(x) for x in sweep.split(",") if x] for G_ in gsweep
                 if not (G_ > 1 and S_ < 2 * G_)]
@@ -540,6 +577,12 @@ def main():
             pt["config"] = cfg_.name
             pt["state"] = {pf.STATE_F32: "f32", pf.STATE_F16: "f16", pf.STATE_F64: "f64"}[st_]
             pt["frac"] = round(pt["updates_per_s"] * (3 * Sb_ + 8) / 1e9 / HBM_PEAK_GBPS, 4)
+            if cfg_.name in ("C4", "C5"):  # batches of two-launch streams: the one-stream PMC pass's bytes per update
+                cb = counter_bytes_per_update(os.path.join(ROOT, "profiles", f"pmc_{cfg_.name.lower()}_n{cfg_.N}.json"),
+                                              cfg_.N)
+                if cb:
+                    pt["counter_bytes_per_update"] = round(cb, 1)
+                    pt["counter_frac"] = round(pt["updates_per_s"] * cb / 1e9 / HBM_PEAK_GBPS, 4)
             multi["points"].append(pt)
 
     exact = None
@@ -577,18 +620,18 @@ def main():
     if rank == 0:
         S = {"f32": 48, "f16": 24, "f64": 96}[state]  # SoA state bytes per particle
         k_mean = float(np.mean(iters)) if iters else 1.0
-        ab = algorithmic_bytes(S, cfg.N, k_mean)
+        ab = algorithmic_bytes(S, cfg.N, float(np.mean(kiters)) if kiters else 1.0)
         roof = None
         timed = {k: v for k, v in stats.items() if v[0] > 0}
         if shape == pf.SHAPE_FRAME2 and "k_frame" in timed:  # PFMPE_K_FRAME times whichever one-launch kernel ran
             timed["k_frame2"] = timed.pop("k_frame")
-        if shape == pf.SHAPE_RESIDENT and "k_frame" in timed:  # the server's frames: k_frame2's body, device-timed
-            timed["k_frame2_srv"] = timed.pop("k_frame")
-            ab["k_frame2_srv"] = ab["k_frame2"]
         wname = {pf.WEIGH_STREAM: "k_weigh_stream", pf.WEIGH_PK: "k_weigh_pk"}.get(weigh_pass)
         if wname and "k_propagate_weigh" in timed:  # the streaming / packed weighing passes
             timed[wname] = timed.pop("k_propagate_weigh")
             ab[wname] = ab["k_propagate_weigh"]
+        if resample_kind == pf.RESAMPLE_OWNERS and "k_resample" in timed:  # the deferred resampling
+            timed["k_resample_owners"] = timed.pop("k_resample")
+            ab["k_resample_owners"] = ab["k_resample"]
         if timed:
             dom = max(timed, key=lambda k: timed[k][1])
             launches, ms = timed[dom]
@@ -603,6 +646,11 @@ def main():
                     "traffic": None if traffic is None else round(traffic),
                     "traffic_source": os.path.relpath(pmc, ROOT) if traffic is not None else None,
                     "bytes_per_launch": ab.get(dom, 0), "avg_us": round(avg_s * 1e6, 3), "launches_timed": launches,
+                    "kernel_pass_frames": kframes,
+                    "avg_us_source": (f"HIP-event dispatch timestamps of every frame of a {kframes}-frame kernel pass "
+                                      f"right after the (unbracketed) timed region: frames {n_frames}..{n_frames + kframes - 1} "
+                                      f"of the stream (scripts/trace_check.py: the same launches in a rocprofv3 trace)"
+                                      if kframes else "HIP-event brackets inside the timed region (--timing-period)"),
                     "per_kernel_avg_us": {k: round(v[1] * 1e3 / v[0], 3) for k, v in timed.items()},
                     "frame_level": {"bytes_per_update": upd_bytes, "achieved": round(frame_gbps, 2),
                                     "frac": round(frame_gbps / HBM_PEAK_GBPS, 4),

@@ -330,26 +330,17 @@ int pfmpe_get_counts(pfmpe_ctx* ctx, uint32_t* out);
  *                                  slot's owner index (4 B) instead of gathering and scattering the particle,
  *                                  and the next frame reads the prior through those indices.
  *                                  Results are bit-identical either way (pfmpe_get_particles gathers)
- *   PFMPE_OPT_RESIDENT      [0|1]  one-launch flat frames (PFMPE_OPT_FUSED 2) through a resident frame server: the
- *                                  k_frame2 blocks stay on the device between frames and take each frame from a
- *                                  pinned mailbox (a doorbell word) instead of a kernel launch.
- *                                  pfmpe_step keeps its blocking contract and results; any other call on the
- *                                  context (read-backs, set_prior, batches, destroy, ...) ends the server first,
- *                                  the next frame starts it again.  A server holds the device's one-launch slot
- *                                  (below) while it runs, and ends by itself after 1 s without a frame.  A frame
- *                                  abandoned at a wait bound is redone by launches, as for PFMPE_OPT_FUSED
  * Within one process at most one one-launch frame runs per device at a time: a context that finds another
  * context's one-launch frame in flight on its device runs that frame as two launches (PFMPE_INFO_GUARD_SKIPS). */
 enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, PFMPE_OPT_FUSED = 4,
        PFMPE_OPT_KEEP_PROPAGATED = 5, PFMPE_OPT_WAIT_BOUND_US = 6, PFMPE_OPT_FUSED_REARM = 7,
-       PFMPE_OPT_MULTI_MAX_BLOCKS = 8, PFMPE_OPT_DEFER_RESAMPLE = 9, PFMPE_OPT_RESIDENT = 10 };
+       PFMPE_OPT_MULTI_MAX_BLOCKS = 8, PFMPE_OPT_DEFER_RESAMPLE = 9 };
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* Context state for monitoring and tests (no reference counterpart: engine introspection). */
 enum { PFMPE_SHAPE_TWO_LAUNCH = 0, /* k_propagate_weigh (+ re-launches) + k_resample + k_resample_final */
        PFMPE_SHAPE_FRAME = 1,      /* k_frame: one launch, tree hand-offs                                */
-       PFMPE_SHAPE_FRAME2 = 2,     /* k_frame2: one launch, flat hand-offs                               */
-       PFMPE_SHAPE_RESIDENT = 3 }; /* k_frame2_srv: the flat frame served by the resident server         */
+       PFMPE_SHAPE_FRAME2 = 2 };   /* k_frame2: one launch, flat hand-offs                               */
 enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 after a fallback)       */
        PFMPE_INFO_FUSED_FALLBACKS = 2,  /* one-launch frames abandoned at the wait bound and redone  */
        PFMPE_INFO_LAST_SHAPE = 3,       /* PFMPE_SHAPE_* of the last step (-1 before the first)      */
@@ -358,13 +349,16 @@ enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 aft
        PFMPE_INFO_LAST_WEIGH_PASS = 6,  /* PFMPE_WEIGH_* of the last two-launch weighing (-1: none)  */
        PFMPE_INFO_LAST_GRID = 7,        /* 1: the last frame's blob table searched its cell grid; 0: the
                                          * x-buckets (no grid for this table or its window; fp64)    */
-       PFMPE_INFO_SERVER_DISPATCHES = 8, /* resident server launches (PFMPE_OPT_RESIDENT)            */
-       PFMPE_INFO_SERVER_FRAMES = 9 };  /* frames the resident server ran                           */
+       PFMPE_INFO_LAST_RESAMPLE = 8 };  /* PFMPE_RESAMPLE_* of the last two-launch resampling (-1: none) */
 /* The two-launch shape's weighing pass: one block per 256 particles (k_propagate_weigh), or
  * resident blocks streaming over them with the next block's state prefetched (k_weigh_stream + k_group +
  * k_top), or the streaming pass with two particles per lane in packed fp32 (k_weigh_pk: 5 markers, fp32 / fp16
  * state, the Philox stream, the blob grid).  All give bit-identical results. */
 enum { PFMPE_WEIGH_BLOCKS = 0, PFMPE_WEIGH_STREAM = 1, PFMPE_WEIGH_PK = 2 };
+/* The two-launch shape's resampling launch: one block per 256 particles with the new prior materialised
+ * (k_resample, then k_resample_final), or, for a deferred frame, one wave per 256-particle block writing owner
+ * indices whose last wave finishes the frame (k_resample_owners).  Same outputs. */
+enum { PFMPE_RESAMPLE_BLOCKS = 0, PFMPE_RESAMPLE_OWNERS = 1 };
 int pfmpe_get_info(const pfmpe_ctx* ctx, int key, int64_t* value);
 
 /* ----------------------------------------------------------------------- device-resident inputs */

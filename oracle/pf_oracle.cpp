@@ -403,9 +403,15 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
   const double accept_thr = (double)((size_t)M * (size_t)std::min(prm->accept_cap, numLED));
   std::vector<double> proj(2 * (size_t)M);
 
+  // fast_search (test speed only) with the Philox stream also spreads the per-particle loop over OpenMP threads:
+  // each particle's draws, pose and likelihood depend on nothing but its own index, every result lands in its own
+  // slot, and the sums below stay sequential, so the outputs are bit-identical to the one-thread loop.  The
+  // reference stream (one sequential engine) and the cpu_baseline timing (fast_search = 0) stay one thread.
+  const bool threaded = prm->fast_search && prm->rng_mode != RNG_REFERENCE;
   do {
-    correspondencesVec.clear();
+    correspondencesVec.assign((size_t)N, std::vector<unsigned>());
     const double g = 1 + prm->growth * std::floor(iter / 10);
+#pragma omp parallel for schedule(static, 4096) if (threaded) firstprivate(PoseParticle_temp, proj)
     for (int n = 0; n < N; ++n) {
       if (n == 0) {
         PoseParticle[n] = current_pose;
@@ -452,7 +458,7 @@ int orc_pf_step(int N, int M, const double* markers /*M x 3*/, const double* K /
       for (int j = 0; j < M; ++j) project2d(K, PoseParticle[n], markers + 3 * j, &proj[2 * j]);
       std::vector<unsigned> pairs;
       probPart[n] = likelihood_literal(M, B, proj.data(), in->blobs, prm->tol, prm->tol_pf, downgrade, pairs);
-      correspondencesVec.push_back(pairs);
+      correspondencesVec[(size_t)n] = std::move(pairs);
     }
     iter++;
     // probPart.maxCoeff(&idx): first maximum

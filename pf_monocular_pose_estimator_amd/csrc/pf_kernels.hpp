@@ -181,6 +181,14 @@ struct alignas(8) CountPart {
 // count << 32 | (2^31 - 1 - index) is the max count at its lowest index; 0 (count 0 at no index) is the identity
 constexpr int kWinShards = 64;
 constexpr int kWinStride = 16;  // keys one 128-B line apart: ~39k block atomics at C4 spread over 64 lines
+// the key area: the key shards, then as many arrival shards of the fused finish (k_resample_owners), each counter at
+// the start of its own 128-B line (one memory-side atomic unit serialises ~25 ns per arrival on one address: one
+// counter for C4's 39k blocks took 400 us)
+constexpr size_t kWinBytes = (size_t)(2 * kWinShards) * kWinStride * sizeof(unsigned long long);
+__host__ __device__ __forceinline__ uint32_t* win_arrive(unsigned long long* winkey) {
+  return (uint32_t*)(winkey + kWinShards * kWinStride);
+}
+constexpr int kArriveStride = 2 * kWinStride;  // uint32 words between arrival shards (128 B)
 __host__ __device__ __forceinline__ unsigned long long win_key(int count, int idx) {
   return ((unsigned long long)(uint32_t)count << 32) | (uint32_t)(0x7fffffff - idx);
 }
@@ -378,7 +386,7 @@ __host__ __device__ __forceinline__ int64_t plane_index(int q, int64_t n, int64_
 }
 
 // the 12 state values of particle n of a state buffer (raw SP values, no anchor / conversion).  POL kPolSc1: the
-// loads bypass L1 (the resident server's prior, written write-through by other workgroups in its previous frame)
+// loads bypass L1
 template <typename SP, int POL = 0>
 __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int64_t ld, int n, SP* v) {
   if constexpr (f16_pairs<SP>()) {
@@ -405,11 +413,10 @@ __device__ __forceinline__ void load_state_raw(const SP* __restrict__ base, int6
     for (int q = 0; q < 12; ++q) v[q] = base[(int64_t)q * ld + n];
   }
 }
-// store 12 raw state values as particle k (WT: write-through, sc1: the resident server's new prior, read by
-// other workgroups in its next frame without a release fence; MI355X_MICROARCH.md "Valid forms")
-template <typename SP, bool WT = false>
+// store 12 raw state values as particle k
+template <typename SP>
 __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t ld, int k, const SP* v) {
-  constexpr int pol = WT ? kPolSc1 : 0;
+  constexpr int pol = 0;
   if constexpr (f16_pairs<SP>()) {
     const __amdgpu_buffer_rsrc_t r = plane_rsrc((const SP*)base, ld);
     const uint32_t pps = (uint32_t)(ld * 4);
@@ -423,11 +430,6 @@ __device__ __forceinline__ void store_state_raw(SP* __restrict__ base, int64_t l
     const uint32_t ps = (uint32_t)(ld * (int64_t)sizeof(SP));
 #pragma unroll
     for (int q = 0; q < 12; ++q) buf_st<pol>(v[q], r, (uint32_t)k * (uint32_t)sizeof(SP), (uint32_t)q * ps);
-  } else if constexpr (WT) {
-#pragma unroll
-    for (int q = 0; q < 12; ++q)
-      __hip_atomic_store((__attribute__((address_space(1))) SP*)(base + (int64_t)q * ld + k), v[q], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
   } else {
 #pragma unroll
     for (int q = 0; q < 12; ++q) base[(int64_t)q * ld + k] = v[q];
@@ -3337,7 +3339,7 @@ struct ResampleLds {
 // finishes the frame.  MODE 2 (k_frame2): the same candidate, then a flat arrival on the sharded count
 // counters; block 0 waits for all of them and finishes.  MODE 0 (k_resample) the block only stores its
 // count partial; k_resample_final finishes.
-template <typename T, int RNG, int MAXM, typename SP, int MODE, bool RAW = false, bool WT = false>
+template <typename T, int RNG, int MAXM, typename SP, int MODE, bool RAW = false>
 __device__ __forceinline__ void resample_phase(
     const FrameArgsT<T>& fa, const LdsConst<T>& sc, const Ctrl& c, Ctrl* __restrict__ ctrl,
     const unsigned char* __restrict__ table, const SP* __restrict__ prior, SP* __restrict__ post, double wd, const T* A,
@@ -3549,7 +3551,7 @@ __device__ __forceinline__ void resample_phase(
           const auto& row = rows[own];
 #pragma unroll
           for (int q = 0; q < 12; ++q) v[q] = RAW ? SP(row.q[q]) : StateIO<T, SP>::store(row.q[q], fa.anc_out[q]);
-          store_state_raw<SP, WT>(post, fa.ld, k, v);
+          store_state_raw<SP>(post, fa.ld, k, v);
         }
       }
     }
@@ -3815,14 +3817,18 @@ template <typename T>
 struct OwnersLds {
   LdsConst<T> sc;  // the frame constants, staged only by the wave holding the most-likely particle
 };
-template <typename T, int RNG, typename SP>
+// before_stores(key): called by the whole wave with the block's winner key (and the most-likely pose written
+// through) before the owner stores are issued (the fused finish publishes the key and arrives there, so its drain
+// does not wait for the owner stores).
+template <typename T, int RNG, typename SP, typename BeforeStores>
 __device__ __forceinline__ void resample_owners_block(const FrameArgsT<T>& fa, const uint32_t* fa_words, int blk,
                                                       const Ctrl& c, const SP* __restrict__ prior,
                                                       const T* __restrict__ wk, __amdgpu_buffer_rsrc_t orsrc,
                                                       const BlockScan* __restrict__ bsk,
                                                       const GroupScan* __restrict__ gscan, uint32_t* __restrict__ counts,
                                                       double* __restrict__ mlpose, OwnersLds<T>& sh, double& carry_R,
-                                                      int& carry_hi, unsigned long long& key) {
+                                                      int& carry_hi, unsigned long long& key,
+                                                      BeforeStores&& before_stores) {
   constexpr int kC = kBlock / 64;
   constexpr uint32_t kDrop = 0x80000000u;  // a buffer offset past num_records: the access is dropped / reads 0
   const int N = fa.N;
@@ -3954,6 +3960,7 @@ __device__ __forceinline__ void resample_owners_block(const FrameArgsT<T>& fa, c
     }
   }
 
+  before_stores(key);
   // Owner indices: particle p of the block owns the slots [ra, re) of its lane and chunk (consecutive, non-empty
   // ranges in particle order).  Each lane writes its own particles' ranges: first 16-B stores of four slots while at
   // least four remain, then single slots; a store past its range goes to an offset the buffer's range check drops
@@ -4029,30 +4036,122 @@ __device__ __forceinline__ void resample_owners_block(const FrameArgsT<T>& fa, c
 #ifndef PFMPE_RESAMPLE_OWNERS_MIN_WAVES
 #define PFMPE_RESAMPLE_OWNERS_MIN_WAVES 6
 #endif
-template <typename T, int RNG, typename SP>
+// The frame's finish in the resampling launch (round 6, VERDICT r05 item 3: no k_resample_final launch after
+// k_resample_owners).  Every wave's winner key goes to a key shard with a memory-side maximum; once it (and the wave's
+// count / most-likely stores) has drained, the wave arrives on arrival shard blk % 64 (no return value: the wave
+// ends).  The wave of the last block, dispatched last (workgroups dispatch in order), finishes the frame: after its
+// own key it polls the 64 arrival shards (one per lane, bounded by the frame's wait bound) until each holds its
+// blocks' count; then it takes the key shards (exchanged with the identity for the next frame, as k_resample_final
+// did) and resets the arrival shards, regenerates the winner's kept pose (the kept set holds stored state values),
+// pairs it (pose_pairs over the blob table in device memory) and writes the record (finalize_frame).  The outputs
+// are k_resample_final's (same functions, same keys).  Per wave LDS: the frame constants, the record image and the
+// pair scratch.
+template <typename T>
+struct OwnersFinalLds {
+  OwnersLds<T> o;
+  OutDev rec;
+  uint32_t ccorr[2 * kMaxMarkers];
+};
+template <typename T, int RNG, int MAXM, typename SP>
+__device__ __forceinline__ void owners_finish(const FrameArgsT<T>& fa, const uint32_t* fa_words, const Ctrl& c,
+                                              Ctrl* __restrict__ ctrl, const SP* __restrict__ prior,
+                                              const unsigned char* __restrict__ table, const double* __restrict__ mlpose,
+                                              unsigned long long* __restrict__ winkey, RecOut* __restrict__ out,
+                                              int32_t seq, uint64_t* __restrict__ stamps, OwnersFinalLds<T>& sh) {
+  const int lane = lane_id();
+  static_assert(kWinShards == 64, "one shard per lane");
+  {  // every other block's arrival (the blocks b < nblk - 1 with b % 64 == lane)
+    uint32_t* sh_arrive = win_arrive(winkey) + lane * kArriveStride;
+    const uint32_t want = lane < fa.nblk - 1 ? (uint32_t)((fa.nblk - 2 - lane) / 64 + 1) : 0u;
+    const uint64_t t0 = rt_now();
+    for (;;) {
+      const bool pend = __hip_atomic_load(sh_arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;
+      if (!__builtin_amdgcn_ballot_w64(pend)) break;
+      if (rt_now() - t0 > fa.wait_ticks) return;  // (no record: the host reports the frame)
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __hip_atomic_store(sh_arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // the next frame's
+  }
+  unsigned long long kmax = __hip_atomic_exchange(winkey + lane * kWinStride, 0ull, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long other = (unsigned long long)__shfl_xor((long long)kmax, o, 64);
+    kmax = other > kmax ? other : kmax;
+  }
+  const int bi = kmax ? 0x7fffffff - (int)(uint32_t)kmax : 0x7fffffff;
+  double ml = 0.0;
+  if (lane < 12) ml = ld_wt_d(mlpose + lane);  // written through by the wave of the most likely particle
+  uint32_t* dst = (uint32_t*)&sh.o.sc;
+  constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
+  for (int i = lane; i < kWordsC; i += 64) dst[i] = fa_words[i];
+  wave_lds_sync();
+  if (stamps && lane == 0) stamps[24] = rt_now();
+  T Pc[12];
+  make_particle<T, RNG, SP>(fa, sh.o.sc, prior, bi, c.kept_iter, Pc);
+  const LdsBlobs<T> tb = view_table<T>(table, fa.B);
+  const uint32_t pl = cand_payload<T, MAXM>(fa, sh.o.sc, tb, Pc, sh.ccorr);
+  if (stamps && lane == 0) stamps[26] = rt_now();
+  finalize_frame<T, RNG, MAXM, SP>(fa, sh.o.sc, c, ctrl, prior, bi, nullptr, mlpose, sh.rec, out, 2 * seq + 1, stamps,
+                                   true, pl, ml);
+  if (stamps && lane == 0) stamps[7] = rt_now();
+}
+// The unfinished and re-init frames (no resampling): block 0's first wave writes the record.
+template <typename T, int RNG, int MAXM, typename SP>
+__device__ __forceinline__ void owners_no_resample(const FrameArgsT<T>& fa, const uint32_t* fa_words, const Ctrl& c,
+                                                   Ctrl* __restrict__ ctrl, const SP* __restrict__ prior,
+                                                   const double* __restrict__ mlpose, RecOut* __restrict__ out,
+                                                   int32_t seq, uint64_t* __restrict__ stamps, OwnersFinalLds<T>& sh) {
+  const int lane = lane_id();
+  if (!c.done) {  // an iteration batch the exit rule has not ended: granule 0 alone, tag 2 * seq (the host goes on)
+    if (lane == 0) st_sys64(&out->g[0], (uint64_t)(uint32_t)(2 * seq) << 32);
+    return;
+  }
+  uint32_t* dst = (uint32_t*)&sh.o.sc;
+  constexpr int kWordsC = (int)(sizeof(LdsConst<T>) / 4);
+  for (int i = lane; i < kWordsC; i += 64) dst[i] = fa_words[i];
+  wave_lds_sync();
+  finalize_frame<T, RNG, MAXM, SP>(fa, sh.o.sc, c, ctrl, prior, -1, nullptr, mlpose, sh.rec, out, 2 * seq + 1, stamps);
+}
+template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_OWNERS_MIN_WAVES))) void
-k_resample_owners(const FrameArgsT<T> fa, const Ctrl* __restrict__ ctrl, const SP* __restrict__ prior,
+k_resample_owners(const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const SP* __restrict__ prior,
                   const T* __restrict__ w0, const T* __restrict__ w1, const BlockScan* __restrict__ bscan0,
                   const BlockScan* __restrict__ bscan1, const GroupScan* __restrict__ gscan,
-                  uint32_t* __restrict__ counts, double* __restrict__ mlpose, unsigned long long* __restrict__ winkey) {
-  __shared__ OwnersLds<T> shw[kWaves];  // per wave: a batch's waves of one workgroup may be different streams
-  OwnersLds<T>& sh = shw[wave_id_u()];
+                  uint32_t* __restrict__ counts, double* __restrict__ mlpose, unsigned long long* __restrict__ winkey,
+                  uint32_t* __restrict__ arrive, const unsigned char* __restrict__ table, RecOut* __restrict__ out,
+                  int32_t seq, uint64_t* __restrict__ stamps) {
+  __shared__ OwnersFinalLds<T> shw[kWaves];  // per wave (a wave never waits for another)
+  OwnersFinalLds<T>& sh = shw[wave_id_u()];
+  const uint32_t* fa_words = (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr();
   const int blk = (int)blockIdx.x * kWaves + wave_id_u();
   if (blk >= fa.nblk) return;
   const Ctrl c = *ctrl;
-  if (!c.done || !c.accepted) return;  // unfinished batch or the re-init branch: k_resample_final writes the record
+  if (!c.done || !c.accepted) {  // unfinished batch or the re-init branch (PE:707-719)
+    if (blk == 0) owners_no_resample<T, RNG, MAXM, SP>(fa, fa_words, c, ctrl, prior, mlpose, out, seq, stamps, sh);
+    return;
+  }
   const __amdgpu_buffer_rsrc_t ors =
       __builtin_amdgcn_make_buffer_rsrc((void*)fa.owner_out, (short)0, fa.N * 4, 0x00020000);
   double carry_R = __longlong_as_double(0x7ff8dead00000000ll);  // a NaN no R equals bitwise: evaluate F(rin)
   int carry_hi = 0;
   unsigned long long key = 0ull;
-  resample_owners_block<T, RNG, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), blk, c, prior,
-                                    c.kept_slot ? w1 : w0, ors, c.kept_slot ? bscan1 : bscan0, gscan, counts, mlpose,
-                                    sh, carry_R, carry_hi, key);
-  // the block's candidate into the sharded winner keys (resample_phase, MODE 0)
-  if (key && lane_id() == 0)
-    __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, key, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  const bool finisher = blk == fa.nblk - 1;
+  // the block's candidate into the sharded winner keys (resample_phase, MODE 0) and, drained with the wave's count
+  // and most-likely stores, the arrival: both before the owner stores, which the finish does not read
+  resample_owners_block<T, RNG, SP>(fa, fa_words, blk, c, prior, c.kept_slot ? w1 : w0, ors,
+                                    c.kept_slot ? bscan1 : bscan0, gscan, counts, mlpose, sh.o, carry_R, carry_hi,
+                                    key, [&](unsigned long long k) {
+                                      if (k && lane_id() == 0)
+                                        __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, k,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                      if (!finisher && lane_id() == 0)
+                                        (void)__hip_atomic_fetch_add(arrive + (blk & (kWinShards - 1)) * kArriveStride,
+                                                                     1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    });
+  if (!finisher) return;
+  owners_finish<T, RNG, MAXM, SP>(fa, fa_words, c, ctrl, prior, table, mlpose, winkey, out, seq, stamps, sh);
 }
 
 // The batched form (pfmpe_step_multi, every stream deferred): wave i of the grid takes the batch's block i, its
@@ -4081,7 +4180,7 @@ k_resample_owners_multi(const StreamDesc<T, SP>* __restrict__ descs, const uint1
   unsigned long long key = 0ull;
   resample_owners_block<T, RNG, SP>(d.fa, (const uint32_t*)&d.fa, blk, c, d.prior, c.kept_slot ? d.w1 : d.w0, ors,
                                     c.kept_slot ? d.bscan1 : d.bscan0, d.gscan, d.counts, d.mlpose, sh, carry_R,
-                                    carry_hi, key);
+                                    carry_hi, key, [](unsigned long long) {});
   if (lane_id() == 0)  // every block has a valid particle, so a key (count 0 included): win_key decoded
     d.cpart[blk] = CountPart{(int32_t)(key >> 32), 0x7fffffff - (int32_t)(uint32_t)key};
 }
@@ -4614,7 +4713,7 @@ __device__ __forceinline__ Ctrl top_math_regs(const FrameArgsT<T>& fa, Ctrl c, i
 #ifndef PFMPE_FRAME2_MIN_WAVES
 #define PFMPE_FRAME2_MIN_WAVES 3
 #endif
-// The LDS of a k_frame2 block (the one-launch kernel and the resident frame server share the body)
+// The LDS of a k_frame2 block
 template <typename T>
 struct Frame2Shared {
   LdsConst<T> sc;
@@ -4623,10 +4722,9 @@ struct Frame2Shared {
   OutDev rec;
   Frame2Lds fl;
 };
-// One frame of k_frame2 for this block.  fa_words: the frame arguments as words (the kernarg segment, or the
-// server's ring slot) for the LDS constants.  Returns false when the block gave up at the weighing barrier's
-// bound (an abandoned frame: no record).  WT: the new prior is stored write-through (the resident server).
-template <typename T, int RNG, int MAXM, bool PRUNE, typename SP, bool WT = false>
+// One frame of k_frame2 for this block.  fa_words: the frame arguments as words (the kernarg segment) for the LDS
+// constants.  Returns false when the block gave up at the weighing barrier's bound (an abandoned frame: no record).
+template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
 __device__ __forceinline__ bool frame2_body(
     const FrameArgsT<T>& fa, const uint32_t* fa_words, const unsigned char* __restrict__ table,
     const SP* __restrict__ prior, SP* __restrict__ post, T* __restrict__ w0, T* __restrict__ w1,
@@ -4648,7 +4746,7 @@ __device__ __forceinline__ bool frame2_body(
   // the prior's loads first: in flight together with the table's, one memory round trip before the weighing
   // instead of two (the table's wait would otherwise come before the prior loads were even issued)
   T A[12];
-  if (valid && n >= 2) load_prior<T, SP, WT ? kPolSc1 : 0>(fa, prior, n, A);
+  if (valid && n >= 2) load_prior(fa, prior, n, A);
   stage_table_consts(table, smem, (size_t)fa.tbytes, fa_words, sc);
   if (threadIdx.x == 0) {
     fl.c = zero_ctrl();  // start of frame: every block keeps an identical copy of the control record
@@ -4827,7 +4925,7 @@ __device__ __forceinline__ bool frame2_body(
   if (valid) wd = have_P ? (double)w : (double)(kslot ? w1 : w0)[n];
   const BlockScan bs = fl.bs[kslot];
   const GroupScan gs = fl.gs;
-  resample_phase<T, RNG, MAXM, SP, 2, false, WT>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec,
+  resample_phase<T, RNG, MAXM, SP, 2>(fa, sc, c, ctrl, table, prior, post, wd, A, P, have_P, bs, gs, rsh, rec,
                                                  tb, cand, mlpose, cpart, nullptr, nullptr, nullptr, counts, out, seq,
                                                  stamps, flat, blk);
   return true;
@@ -4845,217 +4943,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FR
   (void)frame2_body<T, RNG, MAXM, PRUNE, SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), table, prior,
                                              post, w0, w1, part0, part1, ctrl, cpart, flat, counts, cand, mlpose, out,
                                              seq, stamps, smem, S2);
-}
-
-// ---- the resident frame server (PFMPE_OPT_RESIDENT): k_frame2's blocks stay resident across
-// frames and take each frame from a host mailbox instead of a launch.  A one-launch frame at C2 is ~25 us of kernel
-// behind ~10 us of host launch and dispatch (hipLaunchKernel's own ~7 us of host time, then the dispatch of 391
-// blocks); the server replaces that with a doorbell: the host writes the frame's message (the kernel arguments of
-// k_frame2, its buffers, an inline blob table for host blobs) into pinned memory and then the doorbell word.
-//  * Block 0's wave 0 polls the doorbell (system-scope loads of host memory), copies the message into ring slot j
-//    of device memory (one slot per frame of this dispatch: the scalar cache holds no line of a slot before its
-//    frame, so the frame's arguments can be read with scalar loads, as kernel arguments are) and publishes j + 1
-//    (write-through) on a device word, once every block has arrived on the done counter (dseq[kSrvDoneOff]) after the
-//    previous frame.
-//  * Every block's wave 0 polls that word and the done counter, and the block runs frame2_body on the slot.  The
-//    frame reads as its prior the post set other blocks wrote in the previous frame: those stores are write-through
-//    (sc1) and drained before each block's arrival on the done counter, and the prior loads are sc1 loads, so
-//    neither side fences (MI355X_MICROARCH.md "Valid forms", row 1; a release per wave, which writes back the
-//    XCD's whole dirty L2 each time, had the frame take 98 us instead of k_frame2's 30).  Block 0 alone takes an
-//    acquire (its final phase regenerates the winner from the prior with plain loads).
-//  * Every wait is bounded: the doorbell by idle_ticks (then the server exits by itself; the host restarts it
-//    before that can matter, pfmpe_ctx.hpp kSrvIdleNs), the slot word by the same bound, the frame's own barriers
-//    by its wait bound.  A frame abandoned at a barrier sets the exit bit, so every block returns; the host then
-//    finds no record and redoes the frame with launches.  An exit message ends the server (the host's stop), and
-//    the server ends by itself after its last ring slot (the host relaunches it then).
-template <typename T, typename SP>
-struct alignas(256) SrvMsg {
-  FrameArgsT<T> fa;
-  const unsigned char* table;  // the frame's blob table in device memory (bank), or null: inline, after the message
-  const SP* prior;
-  SP* post;
-  // k_frame2's buffers, per message although fixed for a dispatch: read from the slot where the frame uses them
-  // (scalar loads), they are not live across the server's frame loop (as kernel arguments they were hoisted out of
-  // it and spilled)
-  T* w0;
-  T* w1;
-  BlockPart* part0;
-  BlockPart* part1;
-  Ctrl* ctrl;
-  CountPart* cpart;
-  uint32_t* flat;
-  uint32_t* counts;
-  Cand* cand;
-  double* mlpose;
-  RecOut* out;
-  uint64_t* stamps;
-  int32_t exit_;  // 1: the server's exit (srv_stop); read with tinl as one 8-byte word
-  int32_t tinl;   // bytes of the inline table (a multiple of 8; 0: `table`)
-  int32_t seq, pad;
-};
-// host mailbox layout (pinned): the doorbell, the per-frame device durations, the message (+ inline table)
-constexpr int kSrvSlots = 256;                        // frames per server dispatch (ring slots)
-constexpr size_t kSrvDurOff = 256;                    // uint64 dur[kSrvSlots]: s_memrealtime ticks, frame j
-constexpr size_t kSrvMsgOff = kSrvDurOff + 8 * kSrvSlots;
-constexpr uint32_t kSrvExit = 0x80000000u;            // the slot word's exit bit
-constexpr int kSrvDoneOff = 32;                       // dseq[32]: the done counter, 128 B from the slot word
-// Between frames every block's wave 0 polls the slot word: ~0.43 us apart (1,024 cycles), not back to back.  With
-// s_sleep 1 the 390 idle pollers of C2 hammered one line while the frame's last phase ran (the final block took
-// 8 us instead of 1: MI355X_MICROARCH.md, pollers cut chip bandwidth)
-#ifndef PFMPE_SRV_POLL_SLEEP
-#define PFMPE_SRV_POLL_SLEEP 16
-#endif
-constexpr int kSrvPollSleep = PFMPE_SRV_POLL_SLEEP;
-
-// 3 waves per SIMD: two resident blocks per CU next to the occupancy margin, as a one-launch k_frame2 needs
-// (pfmpe_ctx.hpp frame_fused); unconstrained, the frame loop's live state took the server past 168 VGPRs
-#ifndef PFMPE_FRAME2_SRV_MIN_WAVES
-#define PFMPE_FRAME2_SRV_MIN_WAVES 3
-#endif
-// 1: the server's new prior is stored write-through (no release fence per block); 0 (A/B): plain stores and one
-// release fence per block at the end of the frame
-#ifndef PFMPE_SRV_WT
-#define PFMPE_SRV_WT 1
-#endif
-template <typename T, int RNG, int MAXM, bool PRUNE, typename SP>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_FRAME2_SRV_MIN_WAVES))) void k_frame2_srv(
-    const unsigned char* __restrict__ host, unsigned char* __restrict__ ring,
-    const __attribute__((address_space(4))) unsigned char* ring_c, uint32_t slot_bytes, int nslots,
-    uint32_t* __restrict__ dseq, uint32_t idle_ticks, uint64_t* __restrict__ stamps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ Frame2Shared<T> S2;
-  __shared__ int s_exit, s_zero;
-  using Msg = SrvMsg<T, SP>;
-  static_assert(sizeof(Msg) % 256 == 0, "ring slots on whole lines");
-  static_assert(offsetof(Msg, exit_) % 8 == 0 && offsetof(Msg, tinl) == offsetof(Msg, exit_) + 4, "{exit_, tinl} word");
-  auto host_ld = [](const uint64_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-  // every test below is wave-uniform by construction (the wave index through an SGPR, LDS flags through
-  // readfirstlane): the frame loop's index then stays uniform, and with it the slot address whose words the body
-  // reads as scalars
-  const int lane = lane_id(), wv = wave_id_u();
-  uint32_t* done = dseq + kSrvDoneOff;  // the done counter, on a line of its own
-  // every block, wave 0: the done counter holds a count of j * gridDim.x, i.e. every block is through frame j - 1
-  // (bounded; false: expired)
-  auto wait_done = [&](int j, uint64_t t0) {
-    const uint32_t want = (uint32_t)j * gridDim.x;
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      if (rt_now() - t0 > (uint64_t)idle_ticks) return false;
-      __builtin_amdgcn_s_sleep(kSrvPollSleep);
-    }
-    return true;
-  };
-  for (int j = 0; j < nslots; ++j) {
-    unsigned char* slot = ring + (size_t)j * slot_bytes;
-    uint64_t t0 = 0;
-    if (blockIdx.x == 0 && wv == 0) {
-      const uint64_t* bell = (const uint64_t*)host;
-      const uint64_t start = rt_now();
-      bool ok = false;
-      for (;;) {  // bounded: idle_ticks
-        if (host_ld(bell) >= (uint64_t)(j + 1)) {
-          ok = true;
-          break;
-        }
-        if (rt_now() - start > (uint64_t)idle_ticks) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      t0 = rt_now();
-      int quit = 1;
-      if (ok && j > 0) ok = wait_done(j, t0);  // nobody still stores frame j - 1's post set
-      if (ok) {  // the message into the slot, write-through (other XCDs read it), drained before the slot word.
-                 // Every host read of a round is issued before the first is used (one PCIe round trip per round)
-        const uint64_t* src = (const uint64_t*)(host + kSrvMsgOff);
-        uint64_t* dst = (uint64_t*)slot;
-        constexpr int kW = (int)(sizeof(Msg) / 8);
-        constexpr int kR = (kW + 63) / 64;
-        static_assert(kR <= 8, "message words per lane");
-        uint64_t wv8[kR];
-#pragma unroll
-        for (int r = 0; r < kR; ++r) wv8[r] = (lane + 64 * r < kW) ? host_ld(src + lane + 64 * r) : 0ull;
-#pragma unroll
-        for (int r = 0; r < kR; ++r)
-          if (lane + 64 * r < kW) st_wt(dst + lane + 64 * r, wv8[r]);
-        constexpr int kEx = (int)(offsetof(Msg, exit_) / 8);  // {exit_, tinl}
-        const uint64_t ex = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)wv8[kEx / 64], kEx % 64) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(wv8[kEx / 64] >> 32), kEx % 64)
-                             << 32);
-        quit = (int)(uint32_t)ex;
-        const int tw = (int)(uint32_t)(ex >> 32) / 8;
-        for (int i = lane; i < tw; i += 256) {  // the inline table, four reads in flight per lane
-          uint64_t t4[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) t4[r] = (i + 64 * r < tw) ? host_ld(src + kW + i + 64 * r) : 0ull;
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (i + 64 * r < tw) st_wt(dst + kW + i + 64 * r, t4[r]);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (lane == 0)
-        __hip_atomic_store(dseq, (uint32_t)(j + 1) | (quit ? kSrvExit : 0u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (stamps && lane == 0) {  // diagnostic: doorbell seen, slot published (row 0, single writer)
-        stamps[4] = t0;
-        stamps[30] = rt_now();
-      }
-    }
-    if (wv == 0) {  // every block: the slot's word (bounded as the doorbell, plus a margin), then the done count
-      const uint64_t start = rt_now();
-      uint32_t v;
-      for (;;) {
-        v = __hip_atomic_load(dseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v & kSrvExit) || (v & ~kSrvExit) >= (uint32_t)(j + 1)) break;
-        if (rt_now() - start > 2ull * idle_ticks) {
-          v = kSrvExit;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(kSrvPollSleep);
-      }
-      if (!(v & kSrvExit) && j > 0 && !wait_done(j, start)) v = kSrvExit;
-      // The prior loads of the frame body bypass L1 (sc1, WT), so a block needs no acquire for them; block 0 takes
-      // ONE (its finalize regenerates the winner from the prior with plain loads), drained before the barrier
-      if (blockIdx.x == 0 || PFMPE_SRV_WT == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      if (lane == 0) {
-        s_exit = (v & kSrvExit) ? 1 : 0;
-        s_zero = (int)(v & 0u);  // 0, through LDS: the slot's address depends on the wait (below)
-      }
-    }
-    __syncthreads();
-    if (__builtin_amdgcn_readfirstlane(s_exit)) return;
-    // The slot's words as CONSTANT memory (scalar loads, SGPR operands, as kernel arguments): correct because the
-    // slot is written once per dispatch (the scalar cache holds none of its lines before this frame) and before
-    // its word is published; the address depends on the LDS word read after the wait, so no load moves above it.
-    typedef __attribute__((address_space(4))) const Msg CMsg;
-    const CMsg* mc = (const CMsg*)(ring_c + (size_t)j * slot_bytes + __builtin_amdgcn_readfirstlane(s_zero));
-    const Msg* m = (const Msg*)mc;
-    const unsigned char* table = m->tinl ? slot + sizeof(Msg) : m->table;
-    const bool ok = frame2_body<T, RNG, MAXM, PRUNE, SP, PFMPE_SRV_WT != 0>(
-        m->fa, (const uint32_t*)&m->fa, table, m->prior, m->post, m->w0, m->w1, m->part0, m->part1, m->ctrl, m->cpart,
-        m->flat, m->counts, m->cand, m->mlpose, m->out, m->seq, m->stamps, smem, S2);
-    if (!__builtin_amdgcn_readfirstlane((int)ok)) {
-      if (threadIdx.x == 0) __hip_atomic_fetch_or(dseq, kSrvExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;  // abandoned at a barrier: every block leaves (the host redoes the frame with launches)
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0)  // the frame's device time: doorbell seen -> block 0 done (record out)
-      __hip_atomic_store((uint64_t*)(host + kSrvDurOff) + j, rt_now() - t0, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-    // the block's end of frame: every wave's stores drained (the post set went write-through), then ONE arrival
-    // on the done counter for the block (MI355X_MICROARCH.md "Valid forms", row 1; no release fence, which would
-    // write back the XCD's whole dirty L2 once per block)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      // plain post stores (A/B build): one release for the block.  Diagnostic stamps: written back to memory, where
-      // pfmpe_debug_stamps reads them on a side stream while the server runs
-      if (PFMPE_SRV_WT == 0 || stamps) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // ---- state import / export / regeneration (API helpers, not on the timed path).  anchor: the set's

@@ -40,14 +40,17 @@ struct EventPair {
 };
 
 // A batch leader's fence (pfmpe_step_multi), shared by the batch's other contexts until their next work is ordered
-// after the batch; destroyed with the last reference.  The event is recorded on the leader's stream lazily, when a
-// member needs the order (order_after, destroy): a record then captures the batch as well as one right after it
-// would, and a steady multi-stream loop, whose members never use their own streams, records nothing (one record
-// per batch cost 3-5 us of host time per batch).  stream: the leader's stream; null once the leader was destroyed
-// (its destroy drained the stream first, so nothing of the batch is pending then).
+// after the batch; destroyed with the last reference.  The event is recorded on the leader's stream lazily: when a
+// member needs the order (order_after, destroy), or when the leader puts other work on its stream while members
+// still hold the fence (seal_lead_fence, ADVICE r05: a member's read-back then does not wait for the leader's later
+// frames).  A steady multi-stream loop, whose members never use their own streams, records nothing (one record per
+// batch cost 3-5 us of host time per batch).  stream: the leader's stream; null once the leader was destroyed (its
+// destroy drained the stream first, so nothing of the batch is pending then).  recorded: the event holds the end of
+// the fence's latest batch.
 struct BatchFence {
   hipEvent_t ev = nullptr;
   hipStream_t stream = nullptr;
+  bool recorded = false;
   ~BatchFence() {
     if (ev) (void)hipEventDestroy(ev);
   }
@@ -111,36 +114,12 @@ struct pfmpe_ctx {
   int64_t multi_max_blocks = 160000; // PFMPE_OPT_MULTI_MAX_BLOCKS: largest batch this context leads (blocks)
   int last_shape = -1;             // PFMPE_SHAPE_* of the last frame
   int last_weigh_pass = -1;        // PFMPE_WEIGH_* of the last two-launch weighing launch
+  int last_resample = -1;          // PFMPE_RESAMPLE_* of the last two-launch resampling launch
   int64_t guard_skips = 0;         // one-launch frames run as two launches because another was in flight
   std::map<std::pair<const void*, size_t>, int> occ;  // (kernel, LDS bytes) -> blocks per CU
-  // Resident frame server (PFMPE_OPT_RESIDENT): k_frame2_srv stays on the stream between frames
-  // and takes each one-launch frame from the pinned mailbox h_srv (doorbell, per-frame durations, message)
-  bool resident = false;
-  bool srv_alive = false;          // a server dispatch runs on c->stream (and holds fused_inflight)
-  const void* srv_fn = nullptr;    // its kernel, grid, LDS and fixed buffers (a frame that needs others restarts it)
-  int srv_nblk = 0;
-  size_t srv_lds = 0;
-  const void* srv_counts = nullptr;
-  int srv_j = 0;                   // frames rung this dispatch (the doorbell's value)
-  int64_t srv_last_ns = 0;         // host time of its last record (a server idle past kSrvIdleNs is restarted)
-  size_t srv_exit_off = 0;         // mailbox offset of the message's exit word (type-dependent)
-  unsigned char* h_srv = nullptr;  // pinned, host-mapped mailbox
-  unsigned char* hd_srv = nullptr; // its device address
-  size_t srv_bytes = 0;
-  unsigned char* d_srv = nullptr;  // ring: kSrvSlots message slots in HBM
-  size_t srv_slot = 0;
-  uint32_t* d_srv_seq = nullptr;   // slot word [0], done counter [kSrvDoneOff] (256 B)
-  std::vector<uint8_t> srv_timed;  // per ring slot: a timed frame (its duration goes to PFMPE_K_FRAME)
-  int64_t srv_dispatches = 0;
-  int64_t srv_frames = 0;
-  // host-side timing of served frames (undocumented info keys 100-102): record -> next doorbell (host work between
-  // frames), doorbell -> record (the frame as the host sees it), frames counted
-  int64_t srv_host_ns = 0, srv_wait_ns = 0, srv_timed_frames = 0, srv_rec_ns = 0;
   // host-side timing of batches this context leads (undocumented info keys 110-114): entry -> first launch,
   // the launches, last launch -> records, records -> return, batches counted
   int64_t mt_enter = 0, mt_ns[4] = {0, 0, 0, 0}, mt_batches = 0;
-  bool tbl_pending = false;        // h_table holds this frame's table, not yet copied to d_table (resident mode)
-  size_t tbl_bytes = 0;
   Ctrl* d_ctrl = nullptr;
   RecOut* h_rec = nullptr;       // pinned host memory: the record granules, written by the final wave
   RecOut* d_out = nullptr;       // its device address
@@ -159,7 +138,6 @@ struct pfmpe_ctx {
   double* d_xfer = nullptr;      // N x 12 doubles
   uint32_t* d_counts = nullptr;
   uint64_t* d_stamps = nullptr;  // diagnostic stamps (diag & 4)
-  hipStream_t side_stream = nullptr;  // pfmpe_debug_stamps beside a running resident server
   // batch scratch (pfmpe_step_multi, owned by the batch's first context): stream descriptors, the
   // block -> stream map and host-supplied blob tables; the host writes the descriptors and tables into the
   // pinned image, a staging launch (k_stage_multi) moves them to HBM and builds the map
@@ -246,7 +224,10 @@ inline int order_after(pfmpe_ctx* c, hipStream_t to, pfmpe_ctx* err) {
   if (!c->last_stream || c->last_stream == to) return PFMPE_OK;
   if (c->last_fence) {
     if (c->last_fence->stream) {
-      HIPCHK(err, hipEventRecord(c->last_fence->ev, c->last_fence->stream));
+      if (!c->last_fence->recorded) {
+        HIPCHK(err, hipEventRecord(c->last_fence->ev, c->last_fence->stream));
+        c->last_fence->recorded = true;
+      }
       HIPCHK(err, hipStreamWaitEvent(to, c->last_fence->ev, 0));
     }
   } else {
@@ -259,45 +240,21 @@ inline int order_after(pfmpe_ctx* c, hipStream_t to, pfmpe_ctx* err) {
   return PFMPE_OK;
 }
 
-// ---------------------------------------------------------------------- resident frame server (host side)
-// A server idle this long is restarted before its next frame: the kernel ends by itself after kSrvIdleTicks
-// without a doorbell (its clock starts at the record, before the host's), so the host never rings a server that
-// may have left.
-constexpr int64_t kSrvIdleNs = 500000000;       // 0.5 s
-constexpr uint32_t kSrvIdleTicks = 100000000u;  // 1 s of s_memrealtime (100 MHz)
-// Ends the context's server dispatch, if one runs: the exit message through the doorbell, then the stream drains
-// (a server that already left at its idle bound, its last ring slot or an abandoned frame just drains).  The
-// timed frames' device durations are harvested into PFMPE_K_FRAME.  Every C-ABI entry except pfmpe_step calls it
-// (set_device), as does a batch for each member, before any other work goes to the stream.
-inline int srv_stop(pfmpe_ctx* c) {
-  if (!c->srv_alive) return PFMPE_OK;
-  c->srv_alive = false;
-  struct Release {
-    std::atomic<int>& b;
-    ~Release() { b.store(0); }
-  } release{fused_inflight(c->device)};
-  volatile int32_t* ex = (volatile int32_t*)(c->h_srv + c->srv_exit_off);
-  ex[0] = 1;  // exit_
-  ex[1] = 0;  // tinl
-  __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  *(volatile uint64_t*)c->h_srv = (uint64_t)c->srv_j + 1;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  const volatile uint64_t* dur = (const volatile uint64_t*)(c->h_srv + kSrvDurOff);
-  for (int j = 0; j < c->srv_j && j < kSrvSlots; ++j)
-    if (c->srv_timed[j]) {
-      c->k_launches[PFMPE_K_FRAME] += 1;
-      c->k_ms[PFMPE_K_FRAME] += (double)dur[j] * 1e-5;  // 10 ns ticks
-    }
-  c->srv_j = 0;
+// A batch leader about to put other work on its stream while members of its latest batch still hold the fence:
+// record the fence first, so their order_after waits for the batch and not for this later work.
+inline int seal_lead_fence(pfmpe_ctx* c) {
+  BatchFence* f = c->lead_fence.get();
+  if (!f || f->recorded || c->lead_fence.use_count() < 2) return PFMPE_OK;
+  HIPCHK(c, hipEventRecord(f->ev, c->stream));
+  f->recorded = true;
   return PFMPE_OK;
 }
 
-// Every C-ABI entry that enqueues work on the context's own stream starts here: the device, the end of a
-// resident server (pfmpe_step keeps it: keep_server), then the order after the context's latest batch (if any).
-inline int set_device(pfmpe_ctx* c, bool keep_server = false) {
+// Every C-ABI entry that enqueues work on the context's own stream starts here: the device, the leader's fence, then
+// the order after the context's latest batch (if any).
+inline int set_device(pfmpe_ctx* c) {
   HIPCHK(c, hipSetDevice(c->device));
-  if (!keep_server)
-    if (const int r_ = srv_stop(c)) return r_;
+  if (const int r_ = seal_lead_fence(c)) return r_;
   if (const int r_ = order_after(c, c->stream, c)) return r_;
   c->last_stream = c->stream;
   return PFMPE_OK;
@@ -406,9 +363,7 @@ inline int64_t now_ns() {
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (int64_t)ts.tv_sec * 1000000000ll + ts.tv_nsec;
 }
-// deadline_ns (resident frames, whose stream never idles while the server waits for the next doorbell): give up
-// at that host time
-inline int wait_frame(pfmpe_ctx* c, hipStream_t on = nullptr, int64_t deadline_ns = 0) {  // on: the frame's stream
+inline int wait_frame(pfmpe_ctx* c, hipStream_t on = nullptr) {  // on: the frame's stream
   const int32_t want = c->seq;
   int64_t next_query = 0;
   for (uint64_t spin = 0;; ++spin) {
@@ -419,7 +374,6 @@ inline int wait_frame(pfmpe_ctx* c, hipStream_t on = nullptr, int64_t deadline_n
     }
     const int64_t t = now_ns();
     if (next_query == 0) next_query = t + kQueryAfterNs;
-    if (deadline_ns && t >= deadline_ns) return fail(c, PFMPE_E_HIP, "resident frame: no record by its wait bound");
     if (t >= next_query) {
       next_query = t + kQueryAfterNs;
       const hipError_t q = hipStreamQuery(on ? on : c->stream);
@@ -517,7 +471,7 @@ inline int abandoned(pfmpe_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinBytes, c->stream));
   if (c->d_flat) HIPCHK(c, hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->flat_base_w = c->flat_base_c = 0;
@@ -546,14 +500,6 @@ inline BlockPart* gran_part(const pfmpe_ctx* c, int parity) {
   return (BlockPart*)(c->d_gran + (size_t)parity * kGranPartBytes);
 }
 inline CountPart* gran_count(const pfmpe_ctx* c) { return (CountPart*)(c->d_gran + kGranCountOff); }
-
-// resident mode leaves a host-supplied table in h_table (the server takes it inline); any launched frame copies it
-inline int stage_host_table(pfmpe_ctx* c) {
-  if (!c->tbl_pending) return PFMPE_OK;
-  c->tbl_pending = false;
-  HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, c->tbl_bytes, hipMemcpyHostToDevice, c->stream));
-  return PFMPE_OK;
-}
 
 template <typename T, int RNG, int MAXM, typename SP>
 struct Seq {
@@ -654,12 +600,16 @@ struct Seq {
       c->frame_owner_out = c->prior_owner == 0 ? 1 : 0;
       far.owner_out = c->d_owner[c->frame_owner_out];
     }
+    bool owners = false;
     RET(launch_ext(c, PFMPE_K_RESAMPLE, [&] {
-      // a deferred frame: one wave per 256-particle block (k_resample_owners), same outputs
+      // a deferred frame: one wave per 256-particle block (k_resample_owners), same outputs; its
+      // last wave finishes the frame (no k_resample_final)
       if (far.owner_out && !(c->diag & kDiagBlockResample)) {
-        klaunch(c, k_resample_owners<T, RNG, SP>, dim3((unsigned)((fa.nblk + kWaves - 1) / kWaves)), dim3(kBlock), 0,
-                far, (const Ctrl*)c->d_ctrl, prior, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0],
-                c->d_bscan[1], c->d_gscan, c->record_counts ? c->d_counts : nullptr, c->d_mlpose, c->d_winkey);
+        owners = true;
+        klaunch(c, k_resample_owners<T, RNG, MAXM, SP>, dim3((unsigned)((fa.nblk + kWaves - 1) / kWaves)),
+                dim3(kBlock), 0, far, c->d_ctrl, prior, (const T*)c->d_w[0], (const T*)c->d_w[1], c->d_bscan[0],
+                c->d_bscan[1], c->d_gscan, c->record_counts ? c->d_counts : nullptr, c->d_mlpose, c->d_winkey,
+                win_arrive(c->d_winkey), table, c->d_out, seq, c->d_stamps);
         return;
       }
       // the kept-set variant compiles the regeneration path out (its registers spilled in the generic form)
@@ -671,11 +621,13 @@ struct Seq {
                          c->d_stamps, kept ? (const SP*)c->d_prop[0] : nullptr,
                          kept ? (const SP*)c->d_prop[1] : nullptr, c->d_winkey);
     }));
-    RET(launch_ext(c, PFMPE_K_FINAL, [&] {
-      klaunch(c, k_resample_final<T, RNG, MAXM, SP>, dim3(1), dim3(kFinalBlock), BlobTable<T>::bytes(fa.B), fa, c->d_ctrl,
-                         table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0,
-                         c->d_winkey);
-    }));
+    c->last_resample = owners ? PFMPE_RESAMPLE_OWNERS : PFMPE_RESAMPLE_BLOCKS;
+    if (!owners)
+      RET(launch_ext(c, PFMPE_K_FINAL, [&] {
+        klaunch(c, k_resample_final<T, RNG, MAXM, SP>, dim3(1), dim3(kFinalBlock), BlobTable<T>::bytes(fa.B), fa,
+                c->d_ctrl, table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0,
+                c->d_winkey);
+      }));
     RET(wait_frame(c));
     return PFMPE_OK;
   }
@@ -755,162 +707,10 @@ struct Seq {
     return PFMPE_OK;
   }
 
-  // The one-launch frame through the resident server (PFMPE_OPT_RESIDENT): k_frame2's body, the
-  // frame handed over as a mailbox message instead of a launch.  *served = false: not this way (not a flat
-  // one-launch frame, the grid does not fit two blocks per CU, another context's one-launch frame holds the device,
-  // or the frame was abandoned at a wait bound: then the fallback state is set as for a launched frame); the caller
-  // stops the server and runs the frame by launches.
-  template <bool PRUNE>
-  static int frame_resident(pfmpe_ctx* c, const FrameArgsT<T>& fa_in, const unsigned char* table, bool* served) {
-    using Msg = SrvMsg<T, SP>;
-    *served = false;
-    if (!(c->fused == 2 && fa_in.nblk <= kFlatMaxGroups * kGroup && fa_in.gsz == kGroup && c->d_flat)) return PFMPE_OK;
-    const void* fn = (const void*)k_frame2_srv<T, RNG, MAXM, PRUNE, SP>;
-    const size_t need = BlobTable<T>::lds_bytes(fa_in.tbytes);
-    uint32_t* counts = c->record_counts ? c->d_counts : nullptr;
-    if (c->srv_alive && (c->srv_fn != fn || c->srv_nblk != fa_in.nblk || c->srv_lds < need || c->srv_counts != counts ||
-                         c->srv_j >= kSrvSlots || now_ns() - c->srv_last_ns > kSrvIdleNs || c->gframe >= kGranFrames))
-      RET(srv_stop(c));
-    uint32_t gtag = 0;
-    RET(next_gtag(c, &gtag));  // zeroing on wrap goes before a launch: the server was stopped above if it ran
-    if (!c->srv_alive) {
-      // LDS with a margin over this frame's table (the tables of later frames vary), if the grid still fits at
-      // two blocks per CU (frame_fused's residency rule); else exactly this table's
-      size_t lds = (need + need / 4 + 4095) / 4096 * 4096;
-      int per_cu = 0;
-      for (int pass = 0; pass < 2 && per_cu == 0; ++pass, lds = need) {
-        auto key = std::make_pair(fn, lds);
-        auto it = c->occ.find(key);
-        if (it == c->occ.end()) {
-          int occ = 0;
-          HIPCHK(c, hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, kBlock, lds));
-          it = c->occ.emplace(key, occ).first;
-        }
-        per_cu = std::min(2, it->second - 1);
-        if (per_cu < 1 || (int64_t)per_cu * c->num_cu < fa_in.nblk) per_cu = 0;
-        if (per_cu) break;
-      }
-      if (per_cu == 0) return PFMPE_OK;
-      std::atomic<int>& busy = fused_inflight(c->device);
-      int expect = 0;
-      if (!busy.compare_exchange_strong(expect, 1)) {  // another context's one-launch frame is on the device
-        c->guard_skips += 1;
-        return PFMPE_OK;
-      }
-      struct Guard {  // released unless the server starts
-        std::atomic<int>* b;
-        ~Guard() {
-          if (b) b->store(0);
-        }
-      } guard{&busy};
-      const size_t slot = (sizeof(Msg) + BlobTable<T>::max_bytes() + 255) / 256 * 256;
-      if (c->srv_slot != slot) {  // first use: mailbox, ring, slot word
-        if (c->h_srv) HIPCHK(c, hipHostFree(c->h_srv));
-        if (c->d_srv) HIPCHK(c, hipFree(c->d_srv));
-        c->h_srv = c->hd_srv = c->d_srv = nullptr;
-        c->srv_slot = 0;
-        c->srv_bytes = kSrvMsgOff + slot;
-        HIPCHK(c, hipHostMalloc((void**)&c->h_srv, c->srv_bytes, hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(c, hipHostGetDevicePointer((void**)&c->hd_srv, c->h_srv, 0));
-        HIPCHK(c, hipMalloc((void**)&c->d_srv, (size_t)kSrvSlots * slot));
-        if (!c->d_srv_seq) HIPCHK(c, hipMalloc((void**)&c->d_srv_seq, 256));
-        c->srv_slot = slot;
-      }
-      std::memset(c->h_srv, 0, kSrvMsgOff);  // doorbell 0, durations
-      HIPCHK(c, hipMemsetAsync(c->d_srv_seq, 0, 256, c->stream));  // slot word, done counter (kSrvDoneOff)
-      typedef const __attribute__((address_space(4))) unsigned char* ConstRing;
-      hipLaunchKernelGGL((k_frame2_srv<T, RNG, MAXM, PRUNE, SP>), dim3(fa_in.nblk), dim3(kBlock), lds, c->stream,
-                         (const unsigned char*)c->hd_srv, c->d_srv, (ConstRing)c->d_srv, (uint32_t)slot, kSrvSlots,
-                         c->d_srv_seq, kSrvIdleTicks, c->d_stamps);
-      HIPCHK(c, hipGetLastError());
-      guard.b = nullptr;  // held by the server until srv_stop
-      c->srv_alive = true;
-      c->srv_fn = fn;
-      c->srv_nblk = fa_in.nblk;
-      c->srv_lds = lds;
-      c->srv_counts = counts;
-      c->srv_j = 0;
-      c->srv_exit_off = kSrvMsgOff + offsetof(Msg, exit_);
-      c->srv_timed.assign(kSrvSlots, 0);
-      c->srv_dispatches += 1;
-    }
-    // the message (the table inline for host blobs), then the doorbell
-    Msg* m = (Msg*)(c->h_srv + kSrvMsgOff);
-    FrameArgsT<T> a = fa_in;
-    a.flat_base_w = c->flat_base_w;
-    a.flat_base_c = c->flat_base_c;
-    a.gtag = gtag;
-    c->seq = (c->seq + 1) & 0x3fffffff;
-    std::memcpy((void*)&m->fa, (const void*)&a, sizeof(a));
-    m->prior = (const SP*)c->d_state[c->prior_idx];
-    m->post = (SP*)c->d_state[1 - c->prior_idx];
-    m->w0 = (T*)c->d_w[0];
-    m->w1 = (T*)c->d_w[1];
-    m->part0 = gran_part(c, 0);
-    m->part1 = gran_part(c, 1);
-    m->ctrl = c->d_ctrl;
-    m->cpart = gran_count(c);
-    m->flat = c->d_flat;
-    m->counts = counts;
-    m->cand = c->d_cand;
-    m->mlpose = c->d_mlpose;
-    m->out = c->d_out;
-    m->stamps = c->d_stamps;
-    m->seq = c->seq;
-    m->exit_ = 0;
-    const bool inl = c->tbl_pending;
-    if (inl) {
-      std::memcpy(c->h_srv + kSrvMsgOff + sizeof(Msg), c->h_table, c->tbl_bytes);
-      m->table = nullptr;
-      m->tinl = (int32_t)((c->tbl_bytes + 7) / 8 * 8);
-      c->tbl_pending = false;
-    } else {
-      m->table = table;
-      m->tinl = 0;
-    }
-    c->srv_timed[c->srv_j] = c->timing_now ? 1 : 0;
-    c->srv_j += 1;
-    const int64_t t_ring = now_ns();
-    __atomic_store_n((uint64_t*)c->h_srv, (uint64_t)c->srv_j, __ATOMIC_SEQ_CST);
-    *served = true;
-    // the record, bounded by the frame's own waits (weighing and count barriers) plus the idle margin
-    if (wait_frame(c, nullptr, now_ns() + 2 * c->wait_bound_us * 1000 + kSrvIdleNs) != PFMPE_OK) {
-      RET(srv_stop(c));
-      RET(abandoned(c));
-      c->tbl_pending = inl;  // h_table still holds the frame's table: the redone frame copies it
-      *served = false;
-      return PFMPE_OK;
-    }
-    c->srv_last_ns = now_ns();
-    if (c->srv_j > 1 && c->srv_rec_ns) {  // consecutive frames of one dispatch
-      c->srv_host_ns += t_ring - c->srv_rec_ns;
-      c->srv_wait_ns += c->srv_last_ns - t_ring;
-      c->srv_timed_frames += 1;
-    }
-    c->srv_rec_ns = c->srv_last_ns;
-    c->srv_frames += 1;
-    const OutDev& o = *(const OutDev*)c->h_out;
-    c->flat_base_w += (uint32_t)o.iters * (uint32_t)a.nblk;
-    if (o.resampled) c->flat_base_c += (uint32_t)a.nblk;
-    return PFMPE_OK;
-  }
-
   static int step(pfmpe_ctx* c, const FrameArgsT<T>& fa, const unsigned char* table) {
     if (!c->fused && c->fused_user && c->fused_rearm > 0 && c->clean_since_fallback >= c->fused_rearm)
       c->fused = c->fused_user;  // re-armed after enough clean two-launch frames
     const int64_t fallbacks0 = c->fused_fallbacks;
-    if (c->resident && c->fused) {
-      bool served = false;
-      RET(c->prune ? frame_resident<true>(c, fa, table, &served) : frame_resident<false>(c, fa, table, &served));
-      if (served) {
-        if (!frame_done(c)) return fail(c, PFMPE_E_STATE, "resident frame did not finish");
-        c->last_shape = PFMPE_SHAPE_RESIDENT;
-        last_args<T>(c) = fa;
-        return PFMPE_OK;
-      }
-    }
-    RET(srv_stop(c));  // every other path launches on the stream
-    RET(stage_host_table(c));
     if (c->fused) {
       bool launched = false;
       RET(c->prune ? frame_fused<true>(c, fa, table, &launched) : frame_fused<false>(c, fa, table, &launched));
@@ -1177,7 +977,11 @@ struct Seq {
                     dd, db, na, (const uint32_t*)dstat, gen, iter);
         }));
       }
-      for (int i = 0; i < na; ++i) cs[act[i]]->last_weigh_pass = pk ? PFMPE_WEIGH_PK : PFMPE_WEIGH_BLOCKS;
+      for (int i = 0; i < na; ++i) {
+        cs[act[i]]->last_weigh_pass = pk ? PFMPE_WEIGH_PK : PFMPE_WEIGH_BLOCKS;
+        cs[act[i]]->last_resample =
+            all_owners && !(c0->diag & kDiagBlockResample) ? PFMPE_RESAMPLE_OWNERS : PFMPE_RESAMPLE_BLOCKS;
+      }
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
         if (all_owners && !(c0->diag & kDiagBlockResample))  // a wave per block (§4.2d)
           klaunch(c0, k_resample_owners_multi<T, RNG, SP>, dim3((unsigned)((total + kWaves - 1) / kWaves)), dim3(kBlock),
@@ -1361,11 +1165,16 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     HIPCHK(c0, hipEventCreateWithFlags(&f->ev, hipEventDisableTiming));
     f->stream = c0->stream;
     c0->lead_fence = f;
+  } else {
+    // a context of the leader's previous batch that is not in this one: its fence ends before this batch (members of
+    // both batches need no fence: their work stays on this stream; a steady loop of batches records nothing)
+    long held = 0;
+    for (int s = 0; s < S; ++s) held += cs[s]->last_fence.get() == c0->lead_fence.get();
+    if (c0->lead_fence.use_count() - 1 > held) RET(seal_lead_fence(c0));
   }
   // every member's work so far is ordered before the batch (its own stream, or an earlier batch led elsewhere).
   // order_after clears a member's ordering state; if a later member's ordering fails, the earlier ones get their
   // state back (their pending work is still unordered with their own streams)
-  for (int s = 0; s < S; ++s) RET(srv_stop(cs[s]));  // a member's resident server holds its stream
   {
     std::vector<std::pair<hipStream_t, std::shared_ptr<BatchFence>>> saved(S);
     for (int s = 0; s < S; ++s) saved[s] = {cs[s]->last_stream, cs[s]->last_fence};
@@ -1404,6 +1213,7 @@ int multi_m(pfmpe_ctx* const* cs, int S, const pfmpe_frame_in* in) {
     cs[s]->last_stream = c0->stream;
     cs[s]->last_fence = s == 0 ? nullptr : c0->lead_fence;
   }
+  c0->lead_fence->recorded = false;  // this batch is not in the event yet
   return rc;
 }
 

@@ -90,7 +90,7 @@ void free_all(pfmpe_ctx* c) {
   void* dev[] = {c->d_state[0], c->d_state[1], c->d_w[0], c->d_w[1], c->d_prop[0], c->d_prop[1], c->d_part[0], c->d_part[1],
                  c->d_bscan[0], c->d_bscan[1], c->d_gpart[0], c->d_gpart[1], c->d_gscan, c->d_cpart, c->d_winkey,
                  c->d_cgroup, c->d_counters, c->d_ctrl, c->d_gen, c->d_cand, c->d_mlpose, c->d_flat, c->d_roi, c->d_gran, c->d_init, c->d_det, c->d_img, c->d_table, c->d_bank, c->d_xfer, c->d_counts,
-                 c->d_stamps, c->d_owner[0], c->d_owner[1], c->d_srv, c->d_srv_seq};
+                 c->d_stamps, c->d_owner[0], c->d_owner[1]};
   for (void* p : dev)
     if (p) (void)hipFree(p);
   if (c->h_rec) (void)hipHostFree(c->h_rec);
@@ -98,14 +98,12 @@ void free_all(pfmpe_ctx* c) {
   c->h_out = nullptr;
   if (c->h_table) (void)hipHostFree(c->h_table);
   if (c->h_det) (void)hipHostFree(c->h_det);
-  if (c->h_srv) (void)hipHostFree(c->h_srv);
   for (auto& e : c->ev_pool) {
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
   }
   if (c->d_multi) (void)hipFree(c->d_multi);
   if (c->h_multi) (void)hipHostFree(c->h_multi);
-  if (c->side_stream) (void)hipStreamDestroy(c->side_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
 }
 
@@ -237,7 +235,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok &= hipMalloc((void**)&c->d_gscan, (size_t)c->max_grp * sizeof(GroupScan)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_cpart, (size_t)(c->max_blk + 1) * sizeof(CountPart)) == hipSuccess;  // +1: 16-B reads
   ok &= hipMalloc((void**)&c->d_cgroup, (size_t)c->max_grp * sizeof(CountPart)) == hipSuccess;
-  ok &= hipMalloc((void**)&c->d_winkey, kWinShards * kWinStride * sizeof(unsigned long long)) == hipSuccess;
+  ok &= hipMalloc((void**)&c->d_winkey, kWinBytes) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_counters, counters_bytes(c)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_ctrl, sizeof(Ctrl)) == hipSuccess;
   ok &= hipMalloc((void**)&c->d_gen, sizeof(uint32_t)) == hipSuccess;
@@ -269,7 +267,7 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
   ok = ok && hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_flat, 0, kFlatWords * sizeof(uint32_t), c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_gran, 0, kGranBytes, c->stream) == hipSuccess;  // no stale word holds a live tag
-  ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream) == hipSuccess;
+  ok = ok && hipMemsetAsync(c->d_winkey, 0, kWinBytes, c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[0], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipMemsetAsync(c->d_state[1], 0, state_bytes, c->stream) == hipSuccess;
   ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
@@ -281,10 +279,9 @@ int pfmpe_create(pfmpe_ctx** out, int hip_device, int max_particles, int max_mar
 void pfmpe_destroy(pfmpe_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  (void)srv_stop(c);  // the resident server's exit message, else the stream drains only at its idle bound
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->last_fence && c->last_fence->stream) {  // a batch led by another context: its stream up to now
-    if (hipEventRecord(c->last_fence->ev, c->last_fence->stream) == hipSuccess)
+  if (c->last_fence && c->last_fence->stream) {  // a batch led by another context: its stream up to its end
+    if (c->last_fence->recorded || hipEventRecord(c->last_fence->ev, c->last_fence->stream) == hipSuccess)
       (void)hipEventSynchronize(c->last_fence->ev);
     else
       (void)hipStreamSynchronize(c->last_fence->stream);
@@ -367,11 +364,6 @@ int pfmpe_set_option(pfmpe_ctx* c, int option, int64_t value) {
     case PFMPE_OPT_DEFER_RESAMPLE:
       c->defer = value != 0;
       return PFMPE_OK;
-    case PFMPE_OPT_RESIDENT:
-      if (value < 0 || value > 1) return fail(c, PFMPE_E_ARG, "set_option: RESIDENT is 0 or 1");
-      c->resident = value != 0;
-      if (!c->resident) RET(set_device(c));  // ends a running server
-      return PFMPE_OK;
     case PFMPE_OPT_MULTI_MAX_BLOCKS:
       if (value < 1 || value > kMultiMaxBlocks) return fail(c, PFMPE_E_ARG, "set_option: MULTI_MAX_BLOCKS is 1 .. 160000");
       c->multi_max_blocks = value;
@@ -429,7 +421,7 @@ int pfmpe_set_prior(pfmpe_ctx* c, const double* poses, int N) {
     launch_import<float, float>(c, N, c->anchor[c->prior_idx]);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinBytes, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->N = N;
@@ -491,8 +483,7 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* c, const double* blobs, const int32_t* offs
 
 int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
   RET(check_step(c, in, out));
-  RET(set_device(c, /*keep_server=*/true));  // the frame's own path stops it if it launches (Seq::step)
-  c->tbl_pending = false;
+  RET(set_device(c));
   const unsigned char* table = c->d_table;
   const int B = in->B;
   size_t tbytes = 0;
@@ -505,12 +496,7 @@ int pfmpe_step(pfmpe_ctx* c, const pfmpe_frame_in* in, pfmpe_frame_out* out) {
     // the x-bucketed table is built here, O(B), and travels in the same copy the blobs would
     tbytes = build_table(c, in->blobs, B, c->h_table);
     gh = *(const GridHdr*)(c->h_table + grid_off(c, B));
-    if (c->resident) {  // a served frame takes it inline in its message; a launched one copies it (stage_host_table)
-      c->tbl_pending = true;
-      c->tbl_bytes = tbytes;
-    } else {
-      HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
-    }
+    HIPCHK(c, hipMemcpyAsync(c->d_table, c->h_table, tbytes, hipMemcpyHostToDevice, c->stream));
   }
   c->timing_now = c->timing > 0 && (c->timing_frame++ % c->timing) == 0;
   const size_t ev_mark = c->ev_used;  // brackets of earlier frames still pending (harvested lazily)
@@ -755,16 +741,8 @@ int pfmpe_get_counts(pfmpe_ctx* c, uint32_t* out) {
 // Undocumented diagnostic: reset (out == NULL) or read the kStamps stamps of the last frame (diag & 4).
 int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
   if (!c || !c->d_stamps) return PFMPE_E_STATE;
-  // a running resident server keeps the stream: the stamps (written back at each frame's end) go through a side
-  // stream, so steady-state frames can be stamped
+  RET(set_device(c));
   hipStream_t st = c->stream;
-  if (c->srv_alive) {
-    HIPCHK(c, hipSetDevice(c->device));
-    if (!c->side_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking));
-    st = c->side_stream;
-  } else {
-    RET(set_device(c));
-  }
   const size_t rows = 1 + (size_t)c->max_blk;
   if (!out) {
     HIPCHK(c, hipMemsetAsync(c->d_stamps, 0, rows * kStamps * sizeof(uint64_t), st));
@@ -789,10 +767,6 @@ int pfmpe_debug_stamps(pfmpe_ctx* c, uint64_t* out) {
 
 int pfmpe_get_kernel_stats(pfmpe_ctx* c, int kernel, int64_t* launches, double* total_ms) {
   if (!c || kernel < 0 || kernel >= PFMPE_K_COUNT) return PFMPE_E_ARG;
-  if (c->srv_alive) {  // the resident server's frame durations are read once it has ended
-    HIPCHK(c, hipSetDevice(c->device));
-    RET(srv_stop(c));
-  }
   if (c->ev_used) {  // pending brackets of timed frames
     HIPCHK(c, hipSetDevice(c->device));
     RET(harvest_timing(c));
@@ -809,14 +783,10 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
     case PFMPE_INFO_FUSED_FALLBACKS: *value = c->fused_fallbacks; return PFMPE_OK;
     case PFMPE_INFO_LAST_SHAPE: *value = c->last_shape; return PFMPE_OK;
     case PFMPE_INFO_LAST_WEIGH_PASS: *value = c->last_weigh_pass; return PFMPE_OK;
+    case PFMPE_INFO_LAST_RESAMPLE: *value = c->last_resample; return PFMPE_OK;
     case PFMPE_INFO_LAST_GRID: *value = c->last_grid; return PFMPE_OK;
     case PFMPE_INFO_GUARD_SKIPS: *value = c->guard_skips; return PFMPE_OK;
     case PFMPE_INFO_N: *value = c->N; return PFMPE_OK;
-    case PFMPE_INFO_SERVER_DISPATCHES: *value = c->srv_dispatches; return PFMPE_OK;
-    case PFMPE_INFO_SERVER_FRAMES: *value = c->srv_frames; return PFMPE_OK;
-    case 100: *value = c->srv_host_ns; return PFMPE_OK;  // undocumented: resident host timing (diagnostics)
-    case 101: *value = c->srv_wait_ns; return PFMPE_OK;
-    case 102: *value = c->srv_timed_frames; return PFMPE_OK;
     case 110: case 111: case 112: case 113: *value = c->mt_ns[key - 110]; return PFMPE_OK;  // batch host timing
     case 114: *value = c->mt_batches; return PFMPE_OK;
     default: return PFMPE_E_ARG;
@@ -825,10 +795,6 @@ int pfmpe_get_info(const pfmpe_ctx* c, int key, int64_t* value) {
 
 int pfmpe_reset_kernel_stats(pfmpe_ctx* c) {
   if (!c) return PFMPE_E_ARG;
-  if (c->srv_alive) {  // its timed frames belong to the statistics being reset
-    HIPCHK(c, hipSetDevice(c->device));
-    RET(srv_stop(c));
-  }
   if (c->ev_used) {  // pending brackets belong to the statistics being reset
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipEventSynchronize(c->ev_pool[c->ev_used - 1].b));  // before their events are recorded again

@@ -409,7 +409,7 @@ int import_xfer(pfmpe_ctx* c, int N, const double* anchor) {
     import_n<float, float>(c, N, slot);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
-  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinShards * kWinStride * sizeof(unsigned long long), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinBytes, c->stream));
   HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->N = N;

@@ -30,7 +30,7 @@ def main():
     cfg = syn.CONFIGS[a.config]
     st = syn.make_stream(cfg, a.frames)
     rows = run_pair(cfg, a.frames, state, rng)
-    for f, (out, ref, pe, po) in enumerate(rows):
+    for f, (out, ref, pe, po, _) in enumerate(rows):
         T = st.frames[f].truth
         et = lambda p: np.abs(p[[3, 7, 11]] - T[:3, 3]).max()  # noqa: E731
         er = lambda p: rotation_angle(syn.to44(p)[:3, :3], T[:3, :3])  # noqa: E731

@@ -61,7 +61,7 @@ def _engine(N, st, state, rng, prior):
 
 
 def run_pair(cfg, n_frames, state, rng, first_frame_check=None):
-    """Both loops over n_frames; returns per-frame (engine record, oracle record, engine pose, oracle pose)."""
+    """Both loops over n_frames; returns per-frame (engine record, oracle record, engine pose, oracle pose, truth)."""
     st = syn.make_stream(cfg, n_frames)
     prior = st.prior()
     if state != pf.STATE_F64:  # both loops start from the same (float-representable) set
@@ -91,16 +91,22 @@ def run_pair(cfg, n_frames, state, rng, first_frame_check=None):
             te.update(pe, fr.time)
             to.update(po, fr.time)
             o_prior = arr["resampled"]
-            rows.append((out, ref, pe, po))
+            rows.append((out, ref, pe, po, syn.to12(fr.truth)))
     finally:
         eng.close()
     return rows
 
 
 def pose_errors(rows):
-    dt = np.array([np.abs(pe[[3, 7, 11]] - po[[3, 7, 11]]).max() for _, _, pe, po in rows])
-    dr = np.array([rotation_angle(syn.to44(pe)[:3, :3], syn.to44(po)[:3, :3]) for _, _, pe, po in rows])
+    dt = np.array([np.abs(pe[[3, 7, 11]] - po[[3, 7, 11]]).max() for _, _, pe, po, _ in rows])
+    dr = np.array([rotation_angle(syn.to44(pe)[:3, :3], syn.to44(po)[:3, :3]) for _, _, pe, po, _ in rows])
     return dt, dr
+
+
+def truth_distance(pose, truth):
+    """(metres, radians) of a refined pose from the synthetic stream's truth pose of that frame."""
+    return (float(np.abs(pose[[3, 7, 11]] - truth[[3, 7, 11]]).max()),
+            rotation_angle(syn.to44(pose)[:3, :3], syn.to44(truth)[:3, :3]))
 
 
 def assert_within(rows, frac=0.95, tag=""):
@@ -109,6 +115,12 @@ def assert_within(rows, frac=0.95, tag=""):
     miss = np.flatnonzero(~ok)
     print(f"{tag}: {ok.sum()}/{len(rows)} frames within {TOL_T} m / {TOL_R} rad; max dt {dt.max():.3e} m, "
           f"max dr {dr.max():.3e} rad; misses {[(int(f), float(dt[f]), float(dr[f])) for f in miss]}")
+    for f in miss:  # which loop is closer to the truth on a missed frame
+        out, ref, pe, po, truth = rows[f]
+        de, do = truth_distance(pe, truth), truth_distance(po, truth)
+        print(f"{tag}: miss at frame {int(f)}: engine {de[0]:.3e} m / {de[1]:.3e} rad from truth (winner "
+              f"{out['winner_idx']}, weight {out['highest_prob']:.4f}), oracle {do[0]:.3e} m / {do[1]:.3e} rad "
+              f"(winner {ref['winner_idx']}, weight {ref['highest_prob']:.4f})")
     assert ok.sum() >= np.ceil(frac * len(rows)), miss
 
 
@@ -116,7 +128,7 @@ def test_closed_loop_c1_fp64_exact():
     """C1 (BASELINE.json configs[0]: 5 LEDs, 20 blobs, 1000 particles) over 200 frames in the parity mode
     (fp64 state, the reference's minstd stream): every frame's discrete outputs identical, poses to 1e-9."""
     rows = run_pair(syn.CONFIGS["C1"], 200, pf.STATE_F64, pf.RNG_REFERENCE)
-    for f, (out, ref, pe, po) in enumerate(rows):
+    for f, (out, ref, pe, po, _) in enumerate(rows):
         for k in ("iters", "kept_iter", "accepted", "most_likely_idx", "winner_idx", "n_corr", "flag_fail"):
             assert out[k] == ref[k], (f, k, out[k], ref[k])
         assert np.array_equal(out["pairs"], ref["pairs"]), f
@@ -181,3 +193,86 @@ def test_closed_loop_1m_fp16_packed():
     fp64 oracle loop."""
     cfg = syn.StreamConfig("C4s", M=5, B=50, N=1_000_000)
     assert_within(run_pair(cfg, 5, pf.STATE_F16, pf.RNG_PHILOX, _packed_shape), 0.95, "1M fp16 packed")
+
+
+def _stream_shape(eng, out, ref, arr):
+    """C3's production shape: two launches, the streaming 12-marker pass (k_weigh_stream), deferred resampling."""
+    assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
+    assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_STREAM
+    assert out["iters"] == ref["iters"] and out["accepted"] == ref["accepted"]
+
+
+def test_closed_loop_c3_fp64_exact():
+    """C3's shape (BASELINE.json configs[2]: 12 LEDs, 200 heavy-outlier blobs, 1M particles) through the streaming
+    12-marker pass in the parity mode (fp64 state, Philox) over 5 frames: every discrete output identical on every
+    frame, poses to 1e-9 (VERDICT r05 missing 2)."""
+    rows = run_pair(syn.CONFIGS["C3"], 5, pf.STATE_F64, pf.RNG_PHILOX, _stream_shape)
+    for f, (out, ref, pe, po, _) in enumerate(rows):
+        for k in ("iters", "kept_iter", "accepted", "most_likely_idx", "winner_idx", "n_corr", "flag_fail"):
+            assert out[k] == ref[k], (f, k, out[k], ref[k])
+        assert np.array_equal(out["pairs"], ref["pairs"]), f
+        np.testing.assert_allclose(out["winner_pose"], ref["winner_pose"], rtol=0, atol=1e-9, err_msg=str(f))
+    assert_within(rows, 1.0, "C3 fp64")
+
+
+def run_open(cfg, n_frames, state, rng, check=None):
+    """The north_star criterion on identical inputs: one tracker (the oracle's) drives both filters.  Every frame the
+    engine starts from the oracle's resampled set (set_prior; fp32 state rounds it), the oracle tracker's current
+    pose and prediction, and the same blobs; returns per-frame (engine record, oracle record, engine pose, oracle
+    pose, truth), each pose refined from its own winner and pairs."""
+    st = syn.make_stream(cfg, n_frames)
+    prior = st.prior().astype(np.float32).astype(np.float64)
+    eng = _engine(cfg.N, st, state, rng, prior)
+    op = orc.make_params(rng_mode=rng, fast_search=1)
+    to = Tracker(st)
+    rows = []
+    try:
+        for f, fr in enumerate(st.frames):
+            seed = 700 + f
+            if f:
+                eng.set_prior(prior)
+            pm, pp = to.predict(fr.time)
+            out = eng.step(eng.make_frame(to.cur, pp, pm, blobs=fr.blobs, dt=fr.time - to.t_cur, seed=seed,
+                                          frame_idx=f)).as_dict()
+            ref, arr = orc.pf_step(st.markers, st.K, op, prior, to.cur, pp, pm, fr.blobs, dt=fr.time - to.t_cur,
+                                   seed=seed, frame_idx=f)
+            if check:
+                check(eng, out, ref, arr)
+            assert out["accepted"] == 1 and ref["accepted"] == 1, f"frame {f}: track lost (re-init)"
+            pe, _, _ = orc.optimise_pose(st.markers, st.K, fr.blobs, out["pairs"], out["winner_pose"])
+            po, _, _ = orc.optimise_pose(st.markers, st.K, fr.blobs, ref["pairs"], ref["winner_pose"])
+            to.update(po, fr.time)
+            prior = arr["resampled"].astype(np.float32).astype(np.float64) if state == pf.STATE_F32 else arr["resampled"]
+            rows.append((out, ref, pe, po, syn.to12(fr.truth)))
+    finally:
+        eng.close()
+    return rows
+
+
+def test_open_loop_c3_fp32_stream():
+    """C3 (fp32, the production k_weigh_stream<float, 1, 12, true, float> + k_resample_owners) on identical inputs
+    every frame (run_open) over 6 frames, at the 95 % bar.
+
+    A closed loop is not the criterion at C3: its resampling gives each of 1M particles 1-2 of the N stratified
+    targets (N * max w / S = 1.4 on the first frame), so the winner, the first particle of the ~2,600 holding the
+    maximum count of 3, is decided by single targets.  Once one target of an earlier frame lands one particle apart
+    (fp32 against fp64 weights), every later cumulative sum shifts and the two loops follow different, equally good
+    winners: in the round-6 closed loop both stayed 1-7 cm from the truth pose on every frame
+    (profiles/r06/parity_c3.txt).  test_closed_loop_c3_fp32_tracks checks that property."""
+    rows = run_open(syn.CONFIGS["C3"], 6, pf.STATE_F32, pf.RNG_PHILOX, _stream_shape)
+    assert_within(rows, 0.95, "C3 fp32 stream, identical inputs")
+
+
+def test_closed_loop_c3_fp32_tracks():
+    """C3's fp32 closed loop (its own winners fed back) against the oracle's loop: both stay on the target, i.e.
+    the refined pose within 0.15 m / 0.3 rad of the synthetic truth on every frame, and the engine's loop is on
+    average no farther from the truth than the oracle's plus 2 cm (see test_open_loop_c3_fp32_stream for why the
+    two loops separate at C3).  Every frame's distances are printed."""
+    rows = run_pair(syn.CONFIGS["C3"], 6, pf.STATE_F32, pf.RNG_PHILOX, _stream_shape)
+    de = np.array([truth_distance(pe, tr) for _, _, pe, _, tr in rows])
+    do = np.array([truth_distance(po, tr) for _, _, _, po, tr in rows])
+    for f in range(len(rows)):
+        print(f"C3 fp32 closed loop frame {f}: engine {de[f, 0]:.3e} m / {de[f, 1]:.3e} rad, oracle {do[f, 0]:.3e} m / "
+              f"{do[f, 1]:.3e} rad from truth")
+    assert (de[:, 0] < 0.15).all() and (de[:, 1] < 0.3).all()
+    assert de[:, 0].mean() <= do[:, 0].mean() + 0.02

@@ -353,6 +353,43 @@ def test_multi_interleaved_with_single_steps(state):
             e.close()
 
 
+def test_multi_member_after_leader_frames():
+    """after a batch the leader keeps stepping alone (its own frames on the batch stream) while the member
+    still holds the batch's fence; the leader records the fence before its first later frame (seal_lead_fence).  The
+    member's read-back and next frame must then see exactly the batch's result, and a second batch of the same two
+    contexts after that (the fence re-armed) must too.  Every output equals the streams' own pfmpe_step runs."""
+    S, N, frames = 2, 3_000_000, 5
+    streams = _big_streams(S, N, frames, seed0=50)
+    batch = [_big_engine(st, N) for st in streams]
+    solo = [_big_engine(st, N) for st in streams]
+    try:
+        outs = pf.Engine.step_multi(batch, [_big_frame(batch[s], st, 0, s) for s, st in enumerate(streams)])
+        for s in range(S):
+            r = solo[s].step(_big_frame(solo[s], streams[s], 0, s)).as_dict()
+            o = outs[s].as_dict()
+            for k in o:
+                assert np.array_equal(np.asarray(o[k]), np.asarray(r[k])), (s, k)
+        # the member's read-back right after the batch
+        assert _digest(batch[1].get_weights()) == _digest(solo[1].get_weights())
+        for f in (1, 2):  # the leader alone, the member idle
+            a = batch[0].step(_big_frame(batch[0], streams[0], f, 0)).as_dict()
+            b = solo[0].step(_big_frame(solo[0], streams[0], f, 0)).as_dict()
+            assert a["winner_idx"] == b["winner_idx"] and np.array_equal(a["winner_pose"], b["winner_pose"]), f
+        m = batch[1].step(_big_frame(batch[1], streams[1], 1, 1)).as_dict()  # the member's next frame, own stream
+        r = solo[1].step(_big_frame(solo[1], streams[1], 1, 1)).as_dict()
+        assert m["winner_idx"] == r["winner_idx"] and np.array_equal(m["winner_pose"], r["winner_pose"])
+        outs = pf.Engine.step_multi(batch, [_big_frame(batch[0], streams[0], 3, 0), _big_frame(batch[1], streams[1], 2, 1)])
+        ra = solo[0].step(_big_frame(solo[0], streams[0], 3, 0)).as_dict()
+        rb = solo[1].step(_big_frame(solo[1], streams[1], 2, 1)).as_dict()
+        for o, r in zip(outs, (ra, rb)):
+            assert o.as_dict()["winner_idx"] == r["winner_idx"]
+        for s in range(S):
+            assert _digest(batch[s].get_particles(1)) == _digest(solo[s].get_particles(1)), s
+    finally:
+        for e in batch + solo:
+            e.close()
+
+
 @pytest.mark.parametrize("state,rng", [(pf.STATE_F16, pf.RNG_PHILOX), (pf.STATE_F64, pf.RNG_REFERENCE)])
 def test_multi_corrupt_descriptor_is_reported(state, rng):
     """a stream descriptor the device reads differently from what the host wrote is refused

@@ -1,6 +1,8 @@
-"""The production two-launch packed path at full size (C4: 10M fp16, C5: 1M fp32) against the CPU oracle directly.
+"""The production two-launch paths at full size (C3: 1M fp32 12 LEDs, C4: 10M fp16, C5: 1M fp32) against the CPU
+oracle directly.
 
-C4 and C5 frames run k_weigh_pk (two particles per lane, packed fp32; pf_weigh_pk.hpp), which stores each particle's
+C4 and C5 frames run k_weigh_pk (two particles per lane, packed fp32; pf_weigh_pk.hpp), C3 frames the streaming
+12-marker pass k_weigh_stream<float, 1, 12, true, float> (VERDICT r05 missing 2); both store each particle's
 propagated pose in the kept set, then k_resample_owners, whose owner indices make the kept set the next prior.  The
 oracle cannot run a 10M-particle frame, but its Philox draws depend only on (particle, iteration, frame, seed), so
 orc_pf_sample (oracle/pf_oracle.cpp, the motion model PE:543-588 and the literal likelihood PE:2385-2445 of
@@ -12,9 +14,11 @@ range holds k, PE:666-682):
     delta quantum (|pose - anchor| * 2^-10 + 1e-6; the anchor is the frame's current pose, DESIGN.md §4.6);
   * the engine's weight of particle i equals the oracle's literal likelihood within 2e-3 on >= 99.5 % of the
     samples (a marker within ~1e-5 px of the tol_PF gate may flip, DESIGN.md §4.6);
-  * the pass that ran is k_weigh_pk and the frame shape is two launches.
+  * the pass that ran is the production one (k_weigh_pk at C4 / C5, k_weigh_stream at C3) and the frame shape is two
+    launches.
 Frames: a steady frame, an 80-iteration frame (one LED hidden: predictionMatrix composition from iteration 1, noise
-growth from iteration 10, the kept iteration not the last) and an it_since_init = 1 frame (fac = 1 draw ranges).
+growth from iteration 10, the kept iteration not the last; C3's 200 heavy-outlier blobs can satisfy the exit rule
+with 11 LEDs, so its 80 iterations are forced) and an it_since_init = 1 frame (fac = 1 draw ranges).
 """
 import numpy as np
 import pytest
@@ -29,18 +33,19 @@ N_SAMPLES = 2000
 
 
 def _frames(st):
-    """(current pose, predicted pose, prediction, blobs, dt, it_since_init) per frame."""
+    """(current pose, predicted pose, prediction, blobs, dt, it_since_init, force_iters) per frame."""
     out = []
     for f, fr in enumerate(st.frames):
-        cur, pred, blobs, it = np.array(fr.current_pose), np.array(fr.predicted_pose), fr.blobs, 2
+        cur, pred, blobs, it, force = np.array(fr.current_pose), np.array(fr.predicted_pose), fr.blobs, 2, 0
         if f == 1:  # LED 0's blob hidden and particles 0 / 1 5 cm off: 80 iterations, a late iteration kept
             uv0 = syn.project(st.K, fr.truth, st.markers)[0]
             blobs = np.delete(blobs, int(np.argmin(np.sum((blobs - uv0) ** 2, axis=1))), axis=0)
             cur[3] += 0.05
             pred[3] += 0.05
+            force = 80 if st.cfg.heavy else 0
         if f == 2:
             it = 1
-        out.append((cur, pred, np.array(fr.prediction), blobs, fr.dt, it))
+        out.append((cur, pred, np.array(fr.prediction), blobs, fr.dt, it, force))
     return out
 
 
@@ -54,8 +59,9 @@ def owners_from_counts(counts):
     return own[:N]
 
 
-@pytest.mark.parametrize("name,state", [("C5", pf.STATE_F32), ("C4", pf.STATE_F16)])
-def test_packed_path_against_oracle(name, state):
+@pytest.mark.parametrize("name,state,wpass", [("C5", pf.STATE_F32, pf.WEIGH_PK), ("C4", pf.STATE_F16, pf.WEIGH_PK),
+                                              ("C3", pf.STATE_F32, pf.WEIGH_STREAM)])
+def test_packed_path_against_oracle(name, state, wpass):
     cfg = syn.CONFIGS[name]
     N = cfg.N
     st = syn.make_stream(cfg, 3)
@@ -70,13 +76,13 @@ def test_packed_path_against_oracle(name, state):
         eng.set_option(pf.OPT_FUSED, 0)
         eng.set_option(pf.OPT_RECORD_COUNTS, 1)
         eng.set_prior(st.prior(fast=True))
-        for f, (cur, pred, predm, blobs, dt, it) in enumerate(_frames(st)):
+        for f, (cur, pred, predm, blobs, dt, it, force) in enumerate(_frames(st)):
             prior = eng.get_particles(1)  # the prior rows as the engine holds them (fp16: dequantised)
             seed = 3000 + f
             out = eng.step(eng.make_frame(cur, pred, predm, blobs=blobs, dt=dt, seed=seed, frame_idx=f,
-                                          it_since_init=it)).as_dict()
+                                          it_since_init=it, force_iters=force)).as_dict()
             assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
-            assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_PK
+            assert eng.info(pf.INFO_LAST_WEIGH_PASS) == wpass
             assert out["accepted"] == 1 and out["resampled"] == 1, (f, out["flag_fail"])
             if f == 1:
                 assert out["iters"] == 80

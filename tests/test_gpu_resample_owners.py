@@ -172,3 +172,33 @@ def test_owners_batch_equals_block_resample(state):
     assert results[0][1][1]["out"]["iters"] == 80
     for a, b in zip(*results):
         _assert_same(a, b)
+
+
+@pytest.mark.parametrize("state,N,doms", [(pf.STATE_F32, 100_003, (7, 40_000, 99_999)), (pf.STATE_F16, 9_000_000, (5,))])
+def test_owners_dominant_particles(state, N, doms):
+    """the rare branches of resample_owners_block.  Every particle but `doms` sits 0.5 m off the truth
+    (no marker within tol_PF: weight 0), the few at the truth take every target, so each owns a range of tens of
+    thousands of slots or all N: the whole-wave stores of ranges longer than kWide, and at N = 9M (>= 2^23) a count
+    >= 2^23, where the block's winner falls back from the integer key to cmb_max / wave_argmax.  No draw noise, so
+    the ranges are exact.  (The Kt == 0 branch, no target finding a particle, needs a normalised total below every
+    target, which a finite S with an accepted frame never gives: it stays a guard.)"""
+    st = syn.make_stream(syn.StreamConfig("t", M=5, B=50, N=1000), 1)
+    fr = st.frames[0]
+    truth = syn.to12(fr.truth)
+    far = truth.copy()
+    far[3] += 0.5
+    prior = np.tile(far, (N, 1))
+    prior[list(doms)] = truth
+    prm = pf.default_params()
+    prm.ang_min = prm.ang_max = prm.trans_min = prm.trans_max = 0.0
+    ident = np.eye(4)[:3].reshape(12)
+    frames = [(far, far, ident, fr.blobs, 0.02, {"it_since_init": 1})]
+    read = ("p1", "counts")
+    a = _run(N, st.markers, st.K, state, pf.RNG_PHILOX, prior, frames, 0, read=read, params=prm)
+    b = _run(N, st.markers, st.K, state, pf.RNG_PHILOX, prior, frames, pf.DIAG_BLOCK_RESAMPLE, read=read, params=prm)
+    assert a[0]["out"]["accepted"] == 1
+    counts = a[0]["counts"]
+    assert counts.sum() == N and set(np.flatnonzero(counts).tolist()) == set(doms)
+    assert counts.max() > 256 and (N < (1 << 23) or counts.max() >= (1 << 23))
+    assert a[0]["out"]["winner_idx"] == int(np.argmax(counts))
+    _assert_same(a, b)

@@ -1,7 +1,8 @@
 """CPU checks of the resampling test infrastructure (no GPU):
 
-* the oracle's fast_search option (binary search over the running max of the same sequential sums) gives the
-  reference scan's exact counts, indices and new prior (PE:668-682), including negative weights;
+* the oracle's fast_search option (binary search over the running max of the same sequential sums, and with the
+  Philox stream the per-particle loop over OpenMP threads) gives the reference scan's exact counts, indices, weights
+  and new prior (PE:668-682), including negative weights and a multi-threaded 12-marker frame;
 * tests/stratified_ref.py's numpy Philox equals the oracle's Philox4x32-10 (itself pinned by the published
   Random123 vectors in test_oracle_kat.py), and its exact O(N log N) assignment equals the oracle's O(N^2)
   stratified_resample on random weights wherever no target is fragile.
@@ -31,6 +32,26 @@ def test_fast_search_equals_reference_scan(rng):
         for k in ("counts", "resample_idx", "resampled"):
             assert np.array_equal(aa[k], ab[k]), k
         prior = aa["resampled"]
+
+
+def test_fast_search_threads_are_exact():
+    """fast_search with the Philox stream runs the per-particle loop on OpenMP threads: on a 12-marker, 200-blob
+    frame (C3's shape at 8k particles) and on a 12-iteration frame every output equals the one-thread scan's."""
+    cfg = syn.StreamConfig("t", M=12, B=200, N=8_000, heavy=True)
+    st = syn.make_stream(cfg, 2)
+    prior = st.prior()
+    for fr, force in zip(st.frames, (0, 12)):
+        res = []
+        for fast in (0, 1):
+            op = orc.make_params(rng_mode=orc.RNG_PHILOX, fast_search=fast)
+            res.append(orc.pf_step(st.markers, st.K, op, prior, fr.current_pose, fr.predicted_pose, fr.prediction,
+                                   fr.blobs, dt=fr.dt, seed=5 + fr.index, frame_idx=fr.index, force_iters=force))
+        (ra, aa), (rb, ab) = res
+        for k in ra:
+            assert np.array_equal(np.asarray(ra[k]), np.asarray(rb[k])), k
+        for k in aa:
+            assert np.array_equal(aa[k], ab[k]), k
+        assert ra["iters"] == (force or ra["iters"])
 
 
 def test_fast_search_negative_weights():
