@@ -1741,7 +1741,10 @@ struct GridHdr {
   int32_t b0fin, pad;              // blob 0 finite (every table, grid or not)
 };
 static_assert(sizeof(GridHdr) == 48, "grid header");
-constexpr int kGridMaxCells = 2048;   // cell records: 8 KB
+#ifndef PFMPE_GRID_MAX_CELLS
+#define PFMPE_GRID_MAX_CELLS 2048
+#endif
+constexpr int kGridMaxCells = PFMPE_GRID_MAX_CELLS;   // cell records: 8 KB
 constexpr int kGridMaxEntries = 1024; // list entries: 16 KB (B up to ~400 blobs at 2-3 cells each)
 template <typename T>
 struct BlobTable {

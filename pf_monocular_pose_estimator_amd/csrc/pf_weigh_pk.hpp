@@ -302,6 +302,10 @@ __device__ __forceinline__ uint32_t sopaque(uint32_t x) {
   return x;
 }
 
+// 1: k_weigh_pk's self-occlusion test as one packed 16-bit minimum over the marker pairs' key xors (A/B)
+#ifndef PFMPE_PK_DUP_MIN
+#define PFMPE_PK_DUP_MIN 1
+#endif
 // Occupancy floor (waves per SIMD; 1 = the compiler's choice), set by the fp16 / fp32 TUs
 #ifndef PFMPE_WEIGH_PK_MIN_WAVES
 #define PFMPE_WEIGH_PK_MIN_WAVES 1
@@ -518,27 +522,43 @@ __device__ __forceinline__ void weigh_pk_body(const FrameArgsT<float>& fa, const
     // ---- score (score_unordered: B >= M, the host checks), both particles
     f32x2 Pr = pk_splat(0.0f);
     bool accA[MAXM], accB[MAXM];
-    // dup keys: the blob of an accepted marker, a value no blob index takes (0x10000 + j) otherwise; two equal
-    // keys are exactly two accepted markers on one blob (score_unordered's dups > 0)
+    // dup keys: the blob of an accepted marker, a value no blob index takes (0x8000 + j: blob indices are below
+    // kMaxBlobs = 1024) otherwise; two equal keys are exactly two accepted markers on one blob (score_unordered's
+    // dups > 0)
     int kA[MAXM], kB[MAXM];
 #pragma unroll
     for (int j = 0; j < MAXM; ++j) {
       const f32x2 dj = f32x2{sqrt_t(mA[j]), sqrt_t(mB[j])};
       accA[j] = dj.x <= tol_pf;
       accB[j] = dj.y <= tol_pf;
-      kA[j] = accA[j] ? rA[j] : 0x10000 + j;
-      kB[j] = accB[j] ? rB[j] : 0x10000 + j;
+      kA[j] = accA[j] ? rA[j] : 0x8000 + j;
+      kB[j] = accB[j] ? rB[j] : 0x8000 + j;
       const f32x2 q = (pk_splat(tol) - dj) * rtol;
       const f32x2 t = pk_splat(Mt) + q * q;
       Pr = Pr + f32x2{accA[j] ? t.x : 0.0f, accB[j] ? t.y : 0.0f};  // Pr + 0 = Pr (Pr is never -0)
     }
-    // any self-occlusion in the wave: the pairwise key comparisons' lane masks ORed on the scalar unit
+    // any self-occlusion in the wave
+#if PFMPE_PK_DUP_MIN
+    // the keys' pairwise xors as 16-bit halves (A low, B high) folded into one packed 16-bit minimum (k_weigh_pk12's
+    // form): no lane masks live on the scalar unit
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    u16x2 dmin = {0xffff, 0xffff};
+#pragma unroll
+    for (int j = 1; j < MAXM; ++j)
+#pragma unroll
+      for (int e = 0; e < j; ++e)
+        dmin = __builtin_elementwise_min(
+            dmin, __builtin_bit_cast(u16x2, ((uint32_t)(kA[e] ^ kA[j]) & 0xffffu) | ((uint32_t)(kB[e] ^ kB[j]) << 16)));
+    const uint64_t anydup = __builtin_amdgcn_ballot_w64((dmin.x == 0) | (dmin.y == 0));
+#else
+    // the pairwise key comparisons' lane masks ORed on the scalar unit
     uint64_t anydup = 0;
 #pragma unroll
     for (int j = 1; j < MAXM; ++j)
 #pragma unroll
       for (int e = 0; e < j; ++e)
         anydup |= __builtin_amdgcn_ballot_w64(kA[e] == kA[j]) | __builtin_amdgcn_ballot_w64(kB[e] == kB[j]);
+#endif
     float wA = Pr.x, wB = Pr.y;
     if (anydup || fa.downgrade) {  // rare (wave-uniform): the penalties, as score_unordered counts them
       asm volatile("");  // a scalar branch (if-converted, every task paid the counting)
@@ -587,6 +607,303 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WE
   __shared__ PkLds pl;
   weigh_pk_body<SP, false>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x,
                            (int)gridDim.x, table, prior, w0, w1, part0, part1, ctrl, prop0, prop1, iter, smem, sc, pl);
+}
+
+// ---- the packed pass for 12 markers (C3: BASELINE.json configs[2]; round 6).  The task loop,
+// the motion model, the kept-set store and the wave partials are weigh_pk_body's; the likelihood runs over the
+// markers in phases of PH (project2d, the grid's first entries, the rare longer lists, the score terms), so only one
+// phase's projections, cell records and minima are live at a time: five markers' worth fit the 128-VGPR floor, twelve
+// would not.  Every per-marker operation is the 5-marker pass's, hence k_weigh_stream's (column_minima's grid branch,
+// score_unordered's terms, summed in marker order), so the weights, kept set and partials are k_weigh_stream's bit for
+// bit (tests/test_gpu_weigh_pk.py).  Self-occlusion: each marker's key (its blob when accepted, 0x8000 + j otherwise;
+// blob indices < kMaxBlobs = 1024) goes into a 16-bit half of one register per marker, A low, B high; a new marker's
+// key is xored with each earlier one's and the result folded into a packed 16-bit minimum (v_pk_min_u16: both
+// particles per instruction, no lane masks held on the scalar unit, where 66 pairs of ballots spilled), so a zero half
+// at the end means two accepted markers on one blob, and the exact penalty count (score_unordered's) runs only in a
+// wave where some lane has one.
+#ifndef PFMPE_WEIGH_PK12_PHASE
+#define PFMPE_WEIGH_PK12_PHASE 4
+#endif
+#ifndef PFMPE_WEIGH_PK12_FENCE
+#define PFMPE_WEIGH_PK12_FENCE 1
+#endif
+constexpr int kPk12M = 12;
+template <typename SP>
+__device__ __forceinline__ void weigh_pk12_body(const FrameArgsT<float>& fa, const uint32_t* fa_words, int wg, int nwg,
+                                                const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+                                                float* __restrict__ w0, float* __restrict__ w1,
+                                                BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+                                                const Ctrl* __restrict__ ctrl, SP* __restrict__ prop0,
+                                                SP* __restrict__ prop1, int iter, unsigned char* smem,
+                                                LdsConst<float>& sc, PkLds& pl) {
+  constexpr int MAXM = kPk12M, PH = PFMPE_WEIGH_PK12_PHASE;
+  static_assert(MAXM % PH == 0, "whole phases");
+  static_assert(kMaxBlobs <= 0x8000, "blob keys in 16 bits");
+  if (ctrl->done) return;
+  const int slot = ctrl->cur_slot;
+  float* wout = slot ? w1 : w0;
+  SP* pout = slot ? prop1 : prop0;
+  BlockPart* parts = slot ? part1 : part0;
+  const int lane = lane_id();
+  const int ntask = 2 * fa.nblk;
+  const int nwaves = nwg * kWaves;
+  int tk = wg * kWaves + wave_id_u();
+  copy_table(table, smem, (size_t)fa.tbytes);
+  const uint32_t* own = fa.owner;
+  auto rows_of = [&](int t, int& ra, int& rb) {
+    const int n = in_planes(t * 128 + lane, fa.N), m = in_planes(t * 128 + 64 + lane, fa.N);
+    ra = own ? (int)own[n] : n;
+    rb = own ? (int)own[m] : m;
+  };
+  RawState<SP> Ra{}, Rb{};
+  int rA, rB;
+  rows_of(tk, rA, rB);
+  load_state_prefetch<SP>(prior, fa.ld, rA, true, Ra);
+  load_state_prefetch<SP>(prior, fa.ld, rB, true, Rb);
+  rows_of(tk + nwaves, rA, rB);
+  stage_consts_from(fa_words, sc);
+  if (threadIdx.x < 12) {
+    pl.anc_in[threadIdx.x] = fa.anc_in[threadIdx.x];
+    pl.anc_out[threadIdx.x] = fa.anc_out[threadIdx.x];
+  } else if (threadIdx.x == 12) {
+    pl.inv_c = fa.grid.inv_c;
+    pl.ox = fa.grid.ox;
+    pl.oy = fa.grid.oy;
+    pl.fmaxx = fa.grid.fmaxx;
+    pl.fmaxy = fa.grid.fmaxy;
+  }
+  __syncthreads();
+  const LdsBlobs<float> tb = view_table<float>(smem, fa.B);
+  const GridArgs& ga = fa.grid;
+  const unsigned char* cells = tb.base + ga.cell_off;
+  const unsigned char* ents = tb.base + ga.ent_off;
+  const bool predict = fa.it > 1 && (iter % 10) != 0;
+  const float gsc = (float)(1.0 + fa.growth * (double)(iter / 10));
+  const float tol = fa.tol, tol_pf = fa.tol_pf, Mt = (float)MAXM, rtol = rcp_t(fa.tol);
+  for (; tk < ntask; tk += nwaves) {
+    const int nA = tk * 128 + lane, nB = nA + 64;
+    const bool vA = nA < fa.N, vB = nB < fa.N;
+    // ---- motion model (weigh_pk_body's)
+    const Phx2 ph = philox_motion_pair((uint32_t)nA, (uint32_t)nB, (uint32_t)iter | (kTagMotion << 24), fa.flo, fa.fhi,
+                                       fa.key0, fa.key1);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x2 A[12];
+    decode2<SP>(Ra, Rb, pl.anc_in, A);
+    const int64_t ldl = (int64_t)sopaque((uint32_t)fa.ld);
+    load_state_prefetch<SP>(prior, ldl, rA, true, Ra);
+    load_state_prefetch<SP>(prior, ldl, rB, true, Rb);
+    rows_of(tk + 2 * nwaves, rA, rB);
+    f32x2 d[6];
+    {
+      float fa6[6], fb6[6];
+      draw_words(ph.a, fa6);
+      draw_words(ph.b, fb6);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const f32x2 v = f32x2{fa6[q], fb6[q]} - pk_splat(8388608.0f);
+        d[q] = v * sc.rgs[q] + sc.lo[q];
+      }
+    }
+    if (iter >= 10) {
+      asm volatile("");
+#pragma unroll
+      for (int q = 0; q < 6; ++q) d[q] = d[q] * gsc;
+    }
+    if (predict) {
+      f32x2 X[12];
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          f32x2 s = A[i * 4 + 0] * sc.predm[0 * 4 + j];
+          s = pk_fma(A[i * 4 + 1], pk_splat(sc.predm[1 * 4 + j]), s);
+          s = pk_fma(A[i * 4 + 2], pk_splat(sc.predm[2 * 4 + j]), s);
+          if (j == 3) s = s + A[i * 4 + 3];
+          X[i * 4 + j] = s;
+        }
+#pragma unroll
+      for (int q = 0; q < 12; ++q) A[q] = X[q];
+    }
+    f32x2 sa, ca, sb, cb, sz, cz;
+    {
+      auto scs = [&](f32x2 x, f32x2& s, f32x2& c) {
+        const f32x2 x2 = x * x;
+        s = x * pk_fma(x2, pk_splat(-1.0f / 6.0f), pk_splat(1.0f));
+        c = pk_fma(x2, pk_fma(x2, pk_splat(1.0f / 24.0f), pk_splat(-0.5f)), pk_splat(1.0f));
+      };
+      scs(d[0], sa, ca);
+      scs(d[1], sb, cb);
+      scs(d[2], sz, cz);
+    }
+    f32x2 P[12];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const f32x2 a0 = A[i * 4 + 0], a1 = A[i * 4 + 1], a2 = A[i * 4 + 2];
+      const f32x2 z0 = pk_fma(a1, sz, a0 * cz);
+      const f32x2 z1 = pk_fma(a1, cz, a0 * (-sz));
+      const f32x2 y0 = pk_fma(a2, -sb, z0 * cb);
+      const f32x2 y2 = pk_fma(a2, cb, z0 * sb);
+      const f32x2 x1 = pk_fma(y2, sa, z1 * ca);
+      const f32x2 x2 = pk_fma(y2, ca, z1 * (-sa));
+      P[i * 4 + 0] = y0;
+      P[i * 4 + 1] = x1;
+      P[i * 4 + 2] = x2;
+      P[i * 4 + 3] = A[i * 4 + 3] + d[3 + i];
+    }
+    if (tk == 0) {
+#pragma unroll
+      for (int q = 0; q < 12; ++q) P[q].x = lane == 0 ? sc.cur[q] : (lane == 1 ? sc.pred[q] : P[q].x);
+    }
+    if (prop0) {
+      f32x2 D[12];
+      if constexpr (std::is_same<SP, __half>::value) {
+#pragma unroll
+        for (int q = 0; q < 12; ++q) D[q] = P[q] - pk_splat(pl.anc_out[q]);
+      }
+      if (vA) store_kept<SP, 0>(pout, ldl, nA, P, D);
+      if (vB) store_kept<SP, 1>(pout, ldl, nB, P, D);
+    }
+    // ---- project2d's Q = K * P (upper-triangular K), then the markers in phases
+    f32x2 Q[12];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      Q[j] = pk_fma(pk_splat(sc.K[2]), P[8 + j], pk_fma(pk_splat(sc.K[1]), P[4 + j], P[j] * sc.K[0]));
+      Q[4 + j] = pk_fma(pk_splat(sc.K[5]), P[8 + j], P[4 + j] * sc.K[4]);
+      Q[8 + j] = P[8 + j];
+    }
+    f32x2 Pr = pk_splat(0.0f);
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    uint32_t key[MAXM];     // marker j's dup keys, A in the low half, B in the high half
+    u16x2 dmin = {0xffff, 0xffff};  // min over marker pairs of key[e] ^ key[j], per half
+    bool nanA = false, nanB = false;  // marker 0's projection is NaN (Eigen's visitor at coeff(0, 0))
+#pragma unroll
+    for (int p0 = 0; p0 < MAXM; p0 += PH) {
+      f32x2 u[PH], v[PH];
+#pragma unroll
+      for (int i = 0; i < PH; ++i) {
+        const int j = p0 + i;
+        const float X = sc.markers[3 * j], Y = sc.markers[3 * j + 1], Z = sc.markers[3 * j + 2];
+        f32x2 su = Q[0] * X, sv = Q[4] * X, sz2 = Q[8] * X;
+        su = pk_fma(Q[1], pk_splat(Y), su);
+        sv = pk_fma(Q[5], pk_splat(Y), sv);
+        sz2 = pk_fma(Q[9], pk_splat(Y), sz2);
+        su = pk_fma(Q[2], pk_splat(Z), su);
+        sv = pk_fma(Q[6], pk_splat(Z), sv);
+        sz2 = pk_fma(Q[10], pk_splat(Z), sz2);
+        su = su + Q[3];
+        sv = sv + Q[7];
+        sz2 = sz2 + Q[11];
+        const f32x2 rz = f32x2{rcp_t(sz2.x), rcp_t(sz2.y)};
+        u[i] = su * rz;
+        v[i] = sv * rz;
+      }
+      if (p0 == 0) {
+        nanA = __builtin_isunordered(u[0].x, v[0].x);
+        nanB = __builtin_isunordered(u[0].y, v[0].y);
+      }
+      float mA[PH], mB[PH];
+      int rA_[PH], rB_[PH];
+      uint32_t recA[PH], recB[PH];
+#pragma unroll
+      for (int i = 0; i < PH; ++i) {
+        const f32x2 fx = pk_fma(u[i], pk_splat(pl.inv_c), pk_splat(pl.ox));
+        const f32x2 fy = pk_fma(v[i], pk_splat(pl.inv_c), pk_splat(pl.oy));
+        recA[i] = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.x, fy.x);
+        recB[i] = grid_rec(cells, ga.ncx4, pl.fmaxx, pl.fmaxy, fx.y, fy.y);
+      }
+      uint32_t lists = 0;
+#pragma unroll
+      for (int i = 0; i < PH; ++i) {
+        const GridEnt eA = *(const GridEnt*)(ents + (recA[i] & 0xffffu));
+        const GridEnt eB = *(const GridEnt*)(ents + (recB[i] & 0xffffu));
+        const f32x2 dx = f32x2{eA.x, eB.x} - u[i];
+        const f32x2 dy = f32x2{eA.y, eB.y} - v[i];
+        const f32x2 dd = pk_fma(dx, dx, dy * dy);
+        mA[i] = dd.x;
+        mB[i] = dd.y;
+        rA_[i] = eA.orig;
+        rB_[i] = eB.orig;
+        lists |= recA[i] | recB[i];
+      }
+      if (__builtin_amdgcn_ballot_w64(lists > 0x1ffffu)) {  // some lane has a longer list (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < PH; ++i)
+          if (__builtin_amdgcn_ballot_w64((recA[i] > 0x1ffffu) | (recB[i] > 0x1ffffu))) {
+            grid_walk(ents, recA[i], u[i].x, v[i].x, mA[i], rA_[i]);
+            grid_walk(ents, recB[i], u[i].y, v[i].y, mB[i], rB_[i]);
+          }
+      }
+      // the phase's score terms (score_unordered's, in marker order) and dup keys
+#pragma unroll
+      for (int i = 0; i < PH; ++i) {
+        const int j = p0 + i;
+        const f32x2 dj = f32x2{sqrt_t(mA[i]), sqrt_t(mB[i])};
+        const bool accA = dj.x <= tol_pf, accB = dj.y <= tol_pf;
+        const uint32_t kA = accA ? (uint32_t)rA_[i] : 0x8000u + (uint32_t)j;
+        const uint32_t kB = accB ? (uint32_t)rB_[i] : 0x8000u + (uint32_t)j;
+        key[j] = kA | (kB << 16);
+        const f32x2 q = (pk_splat(tol) - dj) * rtol;
+        const f32x2 t = pk_splat(Mt) + q * q;
+        Pr = Pr + f32x2{accA ? t.x : 0.0f, accB ? t.y : 0.0f};
+#pragma unroll
+        for (int e = 0; e < j; ++e)
+          dmin = __builtin_elementwise_min(dmin, __builtin_bit_cast(u16x2, key[e] ^ key[j]));
+      }
+#if PFMPE_WEIGH_PK12_FENCE
+      __builtin_amdgcn_sched_barrier(0);  // one phase's registers at a time (the scheduler would interleave them)
+#endif
+    }
+    const uint64_t anydup = __builtin_amdgcn_ballot_w64((dmin.x == 0) | (dmin.y == 0));
+    float wA = Pr.x, wB = Pr.y;
+    if (anydup || fa.downgrade) {  // rare (wave-uniform): score_unordered's penalty count
+      asm volatile("");
+      auto pen = [&](int sh) {
+        int dups = 0, ndg = 0;
+#pragma unroll
+        for (int j = 0; j < MAXM; ++j) {
+          const uint32_t kj = (key[j] >> sh) & 0xffffu;
+          const bool acc = kj < 0x8000u;
+          bool dup = false;
+#pragma unroll
+          for (int e = 0; e < j; ++e) dup |= (((key[e] >> sh) & 0xffffu) == kj);  // equal keys: both accepted
+          dups += (acc & dup) ? 1 : 0;
+          ndg += (acc && ((fa.downgrade >> j) & 1u)) ? 1 : 0;
+        }
+        return (float)(3 * dups * (dups + 1) / 2 + 2 * ndg);
+      };
+      wA = wA - pen(0);
+      wB = wB - pen(16);
+    }
+    if (nanA) wA = 0.0f;
+    if (nanB) wB = 0.0f;
+    const bool full = (tk + 1) * 128 <= fa.N;
+    if (full) {
+      wout[nA] = wA;
+      wout[nB] = wB;
+    } else {
+      if (!vA) wA = 0.0f;
+      if (!vB) wB = 0.0f;
+      if (vA) wout[nA] = wA;
+      if (vB) wout[nB] = wB;
+    }
+    pk_wave_partial(wA, vA, full, tk * 128, parts + (size_t)tk * 2);
+    pk_wave_partial(wB, vB, full, tk * 128 + 64, parts + (size_t)tk * 2 + 1);
+  }
+}
+
+#ifndef PFMPE_WEIGH_PK12_MIN_WAVES
+#define PFMPE_WEIGH_PK12_MIN_WAVES 3
+#endif
+template <typename SP>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_WEIGH_PK12_MIN_WAVES))) void k_weigh_pk12(
+    const FrameArgsT<float> fa, const unsigned char* __restrict__ table, const SP* __restrict__ prior,
+    float* __restrict__ w0, float* __restrict__ w1, BlockPart* __restrict__ part0, BlockPart* __restrict__ part1,
+    const Ctrl* __restrict__ ctrl, SP* __restrict__ prop0, SP* __restrict__ prop1, int iter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ LdsConst<float> sc;
+  __shared__ PkLds pl;
+  weigh_pk12_body<SP>(fa, (const uint32_t*)__builtin_amdgcn_kernarg_segment_ptr(), (int)blockIdx.x, (int)gridDim.x,
+                      table, prior, w0, w1, part0, part1, ctrl, prop0, prop1, iter, smem, sc, pl);
 }
 
 // ---- batched streams (pfmpe_step_multi): the streaming packed pass for every stream of a batch in ONE launch.

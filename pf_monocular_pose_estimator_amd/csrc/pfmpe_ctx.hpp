@@ -457,10 +457,20 @@ inline bool pk_eligible(const FrameArgsT<float>& fa) {
   return fa.grid.on && fa.grid.b0fin && fa.small_angles && fa.cam_identity && fa.k_upper && fa.M == kExactM &&
          fa.B >= fa.M && !(fa.diag & (kDiagNoPk | kDiagSortedScore));
 }
+// the 12-marker packed pass (k_weigh_pk12, pf_weigh_pk.hpp; C3): the same frames with exactly 12 markers
+template <typename T, int RNG, int MAXM, typename SP>
+constexpr bool kPk12Instance = std::is_same<T, float>::value && RNG == kRngPhilox && MAXM == kPk12M &&
+                               (std::is_same<SP, float>::value || std::is_same<SP, __half>::value);
+inline bool pk12_eligible(const FrameArgsT<float>& fa) {
+  return fa.grid.on && fa.grid.b0fin && fa.small_angles && fa.cam_identity && fa.k_upper && fa.M == kPk12M &&
+         fa.B >= fa.M && !(fa.diag & (kDiagNoPk | kDiagSortedScore));
+}
 template <typename T, int RNG, int MAXM, typename SP>
 inline const void* pk_kernel() {
   if constexpr (kPkInstance<T, RNG, MAXM, SP>)
     return (const void*)k_weigh_pk<SP>;
+  else if constexpr (kPk12Instance<T, RNG, MAXM, SP>)
+    return (const void*)k_weigh_pk12<SP>;
   else
     return nullptr;
 }
@@ -522,6 +532,7 @@ struct Seq {
     // frames it covers (pk_eligible); same outputs, same bits
     bool pk = false;
     if constexpr (kPkInstance<T, RNG, MAXM, SP>) pk = stream && c->prune && pk_eligible(fa);
+    if constexpr (kPk12Instance<T, RNG, MAXM, SP>) pk = stream && c->prune && pk12_eligible(fa);
     c->last_weigh_pass = pk ? PFMPE_WEIGH_PK : (stream ? PFMPE_WEIGH_STREAM : PFMPE_WEIGH_BLOCKS);
     if (stream) {
       const void* fn = pk ? pk_kernel<T, RNG, MAXM, SP>()
@@ -540,6 +551,13 @@ struct Seq {
         if constexpr (kPkInstance<T, RNG, MAXM, SP>) {
           if (pk) {
             klaunch(c, k_weigh_pk<SP>, dim3(grid), dim3(kBlock), lds, fa, table, prior, (float*)c->d_w[0],
+                    (float*)c->d_w[1], c->d_part[0], c->d_part[1], (const Ctrl*)c->d_ctrl, prop0, prop1, iter);
+            return;
+          }
+        }
+        if constexpr (kPk12Instance<T, RNG, MAXM, SP>) {
+          if (pk) {
+            klaunch(c, k_weigh_pk12<SP>, dim3(grid), dim3(kBlock), lds, fa, table, prior, (float*)c->d_w[0],
                     (float*)c->d_w[1], c->d_part[0], c->d_part[1], (const Ctrl*)c->d_ctrl, prop0, prop1, iter);
             return;
           }

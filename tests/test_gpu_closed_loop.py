@@ -196,9 +196,11 @@ def test_closed_loop_1m_fp16_packed():
 
 
 def _stream_shape(eng, out, ref, arr):
-    """C3's production shape: two launches, the streaming 12-marker pass (k_weigh_stream), deferred resampling."""
+    """C3's production shape: two launches, the packed 12-marker pass (k_weigh_pk12; fp64: the streaming pass
+    k_weigh_stream), deferred resampling (k_resample_owners)."""
     assert eng.info(pf.INFO_LAST_SHAPE) == pf.SHAPE_TWO_LAUNCH
-    assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_STREAM
+    assert eng.info(pf.INFO_LAST_WEIGH_PASS) in (pf.WEIGH_PK, pf.WEIGH_STREAM)
+    assert eng.info(pf.INFO_LAST_RESAMPLE) == pf.RESAMPLE_OWNERS
     assert out["iters"] == ref["iters"] and out["accepted"] == ref["accepted"]
 
 
@@ -250,7 +252,7 @@ def run_open(cfg, n_frames, state, rng, check=None):
 
 
 def test_open_loop_c3_fp32_stream():
-    """C3 (fp32, the production k_weigh_stream<float, 1, 12, true, float> + k_resample_owners) on identical inputs
+    """C3 (fp32, the production k_weigh_pk12 + k_resample_owners) on identical inputs
     every frame (run_open) over 6 frames, at the 95 % bar.
 
     A closed loop is not the criterion at C3: its resampling gives each of 1M particles 1-2 of the N stratified

@@ -1,8 +1,8 @@
 """The production two-launch paths at full size (C3: 1M fp32 12 LEDs, C4: 10M fp16, C5: 1M fp32) against the CPU
 oracle directly.
 
-C4 and C5 frames run k_weigh_pk (two particles per lane, packed fp32; pf_weigh_pk.hpp), C3 frames the streaming
-12-marker pass k_weigh_stream<float, 1, 12, true, float> (VERDICT r05 missing 2); both store each particle's
+C4 and C5 frames run k_weigh_pk (two particles per lane, packed fp32; pf_weigh_pk.hpp), C3 frames its 12-marker form
+k_weigh_pk12 (bit-identical to k_weigh_stream<float, 1, 12, true, float>, VERDICT r05 missing 2); both store each particle's
 propagated pose in the kept set, then k_resample_owners, whose owner indices make the kept set the next prior.  The
 oracle cannot run a 10M-particle frame, but its Philox draws depend only on (particle, iteration, frame, seed), so
 orc_pf_sample (oracle/pf_oracle.cpp, the motion model PE:543-588 and the literal likelihood PE:2385-2445 of
@@ -14,8 +14,8 @@ range holds k, PE:666-682):
     delta quantum (|pose - anchor| * 2^-10 + 1e-6; the anchor is the frame's current pose, DESIGN.md §4.6);
   * the engine's weight of particle i equals the oracle's literal likelihood within 2e-3 on >= 99.5 % of the
     samples (a marker within ~1e-5 px of the tol_PF gate may flip, DESIGN.md §4.6);
-  * the pass that ran is the production one (k_weigh_pk at C4 / C5, k_weigh_stream at C3) and the frame shape is two
-    launches.
+  * the pass that ran is the production one (k_weigh_pk at C4 / C5, k_weigh_pk12 at C3; both PFMPE_WEIGH_PK) and the
+    frame shape is two launches.
 Frames: a steady frame, an 80-iteration frame (one LED hidden: predictionMatrix composition from iteration 1, noise
 growth from iteration 10, the kept iteration not the last; C3's 200 heavy-outlier blobs can satisfy the exit rule
 with 11 LEDs, so its 80 iterations are forced) and an it_since_init = 1 frame (fac = 1 draw ranges).
@@ -60,7 +60,7 @@ def owners_from_counts(counts):
 
 
 @pytest.mark.parametrize("name,state,wpass", [("C5", pf.STATE_F32, pf.WEIGH_PK), ("C4", pf.STATE_F16, pf.WEIGH_PK),
-                                              ("C3", pf.STATE_F32, pf.WEIGH_STREAM)])
+                                              ("C3", pf.STATE_F32, pf.WEIGH_PK)])
 def test_packed_path_against_oracle(name, state, wpass):
     cfg = syn.CONFIGS[name]
     N = cfg.N

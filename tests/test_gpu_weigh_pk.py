@@ -1,4 +1,4 @@
-"""k_weigh_pk (two particles per lane, packed fp32; csrc/pf_weigh_pk.hpp) against k_weigh_stream.
+"""k_weigh_pk / k_weigh_pk12 (two particles per lane, packed fp32; csrc/pf_weigh_pk.hpp) against k_weigh_stream.
 
 The packed pass must give the same bits as the one-particle-per-lane streaming pass it replaces (every fp32
 operation is the same operation in each lane of a v_pk_* instruction): the frame records, the weights, the
@@ -9,7 +9,9 @@ cases the pass has code for:
     predictionMatrix composition from iteration 1, the noise growth from iteration 10, the kept slot moving);
   * it_since_init = 1 (no prediction, fac = 1 draw ranges);
   * downgraded markers and self-occlusion (two markers 1 mm apart, one blob for both): the penalty branch;
-  * the kept propagated set on (one-stream default) and off (regeneration in k_resample).
+  * the kept propagated set on (one-stream default) and off (regeneration in k_resample);
+  * 12 markers (k_weigh_pk12, C3's pass): heavy clutter (200 blobs with near outliers, longer grid lists), the
+    80-iteration frame, penalties with two marker pairs on shared blobs and downgraded markers.
 The pass is also checked to be the one that ran (PFMPE_INFO_LAST_WEIGH_PASS).
 """
 import numpy as np
@@ -107,9 +109,51 @@ def test_pk_pass_penalties(state):
     _assert_same(a, b)
 
 
+@pytest.mark.parametrize("state", [pf.STATE_F16, pf.STATE_F32])
+def test_pk12_pass_is_bit_identical(state):
+    """The 12-marker packed pass against k_weigh_stream<float, 1, 12>: C3's clutter (200 blobs, near and far
+    outliers), N not a multiple of 128, the steady / 80-iteration (forced: the clutter can satisfy the exit rule with
+    11 LEDs) / it_since_init = 1 frames."""
+    N = 1_000_033
+    st = syn.make_stream(syn.StreamConfig("t", M=12, B=200, N=N, heavy=True), 3)
+    frames = _frames(st)
+    frames[1] = (frames[1][0], frames[1][1], {"force_iters": 80})
+    a, pa = _run(st, N, state, pf.DIAG_FORCE_STREAM, frames)
+    b, pb = _run(st, N, state, pf.DIAG_FORCE_STREAM | pf.DIAG_NO_PK, frames)
+    assert pa == [pf.WEIGH_PK] * 3 and pb == [pf.WEIGH_STREAM] * 3, (pa, pb)
+    assert a[1]["out"]["iters"] == 80
+    _assert_same(a, b)
+
+
+@pytest.mark.parametrize("state", [pf.STATE_F16, pf.STATE_F32])
+def test_pk12_pass_penalties(state):
+    """12 markers with self-occlusion in two places (marker 11 beside marker 10, marker 5 beside marker 2, each
+    pair sharing one blob: dups = 2, the 3 * s * (s + 1) / 2 penalty) and downgraded markers 1, 7 and 10."""
+    N = 300_001
+    st = syn.make_stream(syn.StreamConfig("t", M=12, B=200, N=N, heavy=True), 2)
+    markers = np.array(st.markers, dtype=np.float64).copy()
+    markers[11] = markers[10] + np.array([0.001, 0.0, 0.0])
+    markers[5] = markers[2] + np.array([0.0, 0.001, 0.0])
+    frames = []
+    for fr in st.frames:
+        uv = syn.project(st.K, fr.truth, markers)
+        blobs = fr.blobs.copy()
+        for a_, b_ in ((11, 10), (5, 2)):
+            i = int(np.argmin(np.sum((blobs - uv[a_]) ** 2, axis=1)))
+            blobs[i] = uv[b_]
+        frames.append((fr, blobs, {}))
+    dg = np.zeros(12, dtype=np.uint8)
+    dg[[1, 7, 10]] = 1
+    a, pa = _run(st, N, state, pf.DIAG_FORCE_STREAM, frames, markers=markers, downgrade=dg)
+    b, pb = _run(st, N, state, pf.DIAG_FORCE_STREAM | pf.DIAG_NO_PK, frames, markers=markers, downgrade=dg)
+    assert pa == [pf.WEIGH_PK] * 2 and pb == [pf.WEIGH_STREAM] * 2, (pa, pb)
+    _assert_same(a, b)
+
+
 def test_pk_pass_default_at_c4_c5():
-    """The default two-launch weighing pass at C4 / C5 (fp16 / fp32, 5 markers, 50 blobs) is k_weigh_pk."""
-    for name, state in (("C5", pf.STATE_F32), ("C4", pf.STATE_F16)):
+    """The default two-launch weighing pass at C4 / C5 (fp16 / fp32, 5 markers, 50 blobs) is k_weigh_pk, and at C3
+    (fp32, 12 markers, 200 blobs) k_weigh_pk12 (both report PFMPE_WEIGH_PK)."""
+    for name, state in (("C5", pf.STATE_F32), ("C4", pf.STATE_F16), ("C3", pf.STATE_F32)):
         cfg = syn.CONFIGS[name]
         st = syn.make_stream(cfg, 1)
         fr = st.frames[0]
