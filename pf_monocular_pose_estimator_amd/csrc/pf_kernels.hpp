@@ -1741,10 +1741,17 @@ struct GridHdr {
   int32_t b0fin, pad;              // blob 0 finite (every table, grid or not)
 };
 static_assert(sizeof(GridHdr) == 48, "grid header");
-#ifndef PFMPE_GRID_MAX_CELLS
-#define PFMPE_GRID_MAX_CELLS 2048
+// The cell budget of a table's grid: the coarse one (2,048 cells, 8 KB of records) for ordinary blob counts, the 4x
+// finer one (8,192, 32 KB) from kGridFineMinBlobs blobs (C3's 200 with clutter), whose cell lists are otherwise long
+// enough that most waves walk them: measured (profiles/r06/ab_grid_cells.txt) C3 weighing 56.5 -> 50.8 us with the
+// fine grid, while at 50 blobs (C2 / C4 / C5) its larger table copy costs 1.5-1.8 us per frame.  A fine grid over the
+// entry budget falls back to the coarse one, then to the x-buckets.
+constexpr int kGridMaxCells = 8192;   // cell records: 32 KB
+constexpr int kGridCoarseCells = 2048;
+#ifndef PFMPE_GRID_FINE_MIN_BLOBS
+#define PFMPE_GRID_FINE_MIN_BLOBS 128
 #endif
-constexpr int kGridMaxCells = PFMPE_GRID_MAX_CELLS;   // cell records: 8 KB
+constexpr int kGridFineMinBlobs = PFMPE_GRID_FINE_MIN_BLOBS;
 constexpr int kGridMaxEntries = 1024; // list entries: 16 KB (B up to ~400 blobs at 2-3 cells each)
 template <typename T>
 struct BlobTable {
@@ -1869,10 +1876,11 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
     bx0 = std::min(bx0, x), bx1 = std::max(bx1, x), by0 = std::min(by0, y), by1 = std::max(by1, y);
   }
   const double gx0 = bx0 - m, gy0 = by0 - m, w = bx1 - bx0 + 2 * m, h = by1 - by0 + 2 * m;
+  for (int budget = B >= kGridFineMinBlobs ? kGridMaxCells : kGridCoarseCells;; budget = kGridCoarseCells) {
   // square cells: at least the window (2m) and few enough for the cell budget
-  double cs = std::max(2.0 * m, std::sqrt(w * h / (double)kGridMaxCells));
+  double cs = std::max(2.0 * m, std::sqrt(w * h / (double)budget));
   int ncx = (int)std::ceil(w / cs), ncy = (int)std::ceil(h / cs);
-  while ((int64_t)ncx * ncy > kGridMaxCells) {
+  while ((int64_t)ncx * ncy > budget) {
     cs *= 1.0625;
     ncx = (int)std::ceil(w / cs);
     ncy = (int)std::ceil(h / cs);
@@ -1922,7 +1930,11 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
           }
         }
     }
-    if (pass == 0 && nent > kGridMaxEntries) return total;  // too many entries: the x-buckets serve
+    if (pass == 0 && nent > kGridMaxEntries) break;  // too many entries: a coarser grid, then the x-buckets
+  }
+  if (nent > kGridMaxEntries) {
+    if (budget == kGridCoarseCells) return total;
+    continue;
   }
   uint32_t* cell = (uint32_t*)((unsigned char*)gh + sizeof(GridHdr));
   for (int c = 0; c < ncell; ++c) {  // an empty cell points at the sentinel (byte offset 0)
@@ -1942,6 +1954,7 @@ inline size_t build_blob_table_host(const double* blobs, int B, double tolq, uns
   gh->ncell = ncell;
   gh->nent = nent;
   return BlobTable<T>::total_bytes(B, ncell, nent);
+  }
 }
 
 // block-wide copy of the table into LDS (16-byte words); callers barrier before use

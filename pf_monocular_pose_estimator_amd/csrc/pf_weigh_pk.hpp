@@ -829,6 +829,7 @@ __device__ __forceinline__ void weigh_pk12_body(const FrameArgsT<float>& fa, con
 #pragma unroll
         for (int i = 0; i < PH; ++i)
           if (__builtin_amdgcn_ballot_w64((recA[i] > 0x1ffffu) | (recB[i] > 0x1ffffu))) {
+            // (one loop over both particles' entries measured slower: C3 weighing 56.5 -> 59.6 us)
             grid_walk(ents, recA[i], u[i].x, v[i].x, mA[i], rA_[i]);
             grid_walk(ents, recB[i], u[i].y, v[i].y, mB[i], rB_[i]);
           }
