@@ -2068,7 +2068,10 @@ __device__ __forceinline__ GroupScan load_gscan_wt(const GroupScan* p) {
 // W4 (k_group after the streaming pass): `part` holds kWaves wave partials per block (BlockPart fields: wave
 // total, max / min in-wave prefix, max / argmax, min / argmin), combined here into the block partial with
 // publish_iteration's association (((0 + t0) + t1) + ..., the running extrema of pre + prefix, waves in order).
-template <bool W4 = false>
+// W4: the partials are wave partials (four per block, the streaming passes); SC1 (with W4): written in this launch
+// by other waves (8-B agent-scope stores, drained before their arrivals: the fused tail of the packed passes), so
+// read with 8-B agent-scope loads (MI355X_MICROARCH.md "Valid forms": 8-B agent atomics both sides)
+template <bool W4 = false, bool SC1 = false>
 __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, const BlockPart* __restrict__ part,
                                                      BlockScan* __restrict__ bscan, GroupPart* __restrict__ gpart) {
   const int lane = lane_id();
@@ -2084,8 +2087,22 @@ __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, c
     if (vb && W4) {  // written by the previous launch: plain loads
       const BlockPart* p = part + (size_t)b * kWaves;
       BlockPart w[kWaves];
+      if constexpr (SC1) {
 #pragma unroll
-      for (int ww = 0; ww < kWaves; ++ww) w[ww] = p[ww];
+        for (int ww = 0; ww < kWaves; ++ww) {
+          w[ww].sum = ld_wt_d(&p[ww].sum);
+          w[ww].maxrel = ld_wt_d(&p[ww].maxrel);
+          w[ww].minrel = ld_wt_d(&p[ww].minrel);
+          w[ww].maxw = ld_wt_d(&p[ww].maxw);
+          w[ww].minw = ld_wt_d(&p[ww].minw);
+          const uint64_t ai = ld_wt(&p[ww].argmax);
+          w[ww].argmax = lo32(ai);
+          w[ww].argmin = hi32(ai);
+        }
+      } else {
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) w[ww] = p[ww];
+      }
       double pre = 0.0, bmx = w[0].maxw, bmn = w[0].minw;
       int bix = w[0].argmax, bin = w[0].argmin;
 #pragma unroll
@@ -2971,6 +2988,7 @@ struct alignas(16) StreamDesc {  // 16-B multiple: k_stage_multi copies 16-B wor
   Cand* cand;
   double* mlpose;
   RecOut* out;
+  unsigned long long* winkey;  // the stream's winner keys and arrival shards (k_resample_owners_multi's finish)
   int32_t seq;
   int32_t first_blk;  // the stream's first block in the grid
   int32_t wg;         // resident workgroups of the stream in a streaming batched weighing pass (k_weigh_pk_multi)
@@ -4171,15 +4189,15 @@ k_resample_owners(const FrameArgsT<T> fa, Ctrl* __restrict__ ctrl, const SP* __r
 }
 
 // The batched form (pfmpe_step_multi, every stream deferred): wave i of the grid takes the batch's block i, its
-// stream from the block map (batch_block's checks, per wave).  Batches keep the count partials k_resample_final_multi
-// reduces (no winner keys): the wave's candidate goes to its block's partial.
-template <typename T, int RNG, typename SP>
+// stream from the block map (batch_block's checks, per wave), and each stream is finished as one stream is
+// (k_resample_owners' keys, arrival shards and finisher, on the stream's own key area): no k_resample_final_multi.
+template <typename T, int RNG, int MAXM, typename SP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(PFMPE_RESAMPLE_OWNERS_MIN_WAVES))) void
 k_resample_owners_multi(const StreamDesc<T, SP>* __restrict__ descs, const uint16_t* __restrict__ bmap, int S,
                         const uint32_t* __restrict__ status, uint32_t gen, int total) {
-  __shared__ OwnersLds<T> shw[kWaves];  // per wave: the workgroup's waves may belong to different streams, each
-                                         // staging its own stream's constants for its most-likely particle
-  OwnersLds<T>& sh = shw[wave_id_u()];
+  __shared__ OwnersFinalLds<T> shw[kWaves];  // per wave: the workgroup's waves may belong to different streams, each
+                                              // staging its own stream's constants
+  OwnersFinalLds<T>& sh = shw[wave_id_u()];
   const int gb = (int)blockIdx.x * kWaves + wave_id_u();
   if (gb >= total) return;
   const int s = __builtin_amdgcn_readfirstlane((int)bmap[gb]);
@@ -4188,17 +4206,33 @@ k_resample_owners_multi(const StreamDesc<T, SP>* __restrict__ descs, const uint1
   const int blk = gb - __builtin_amdgcn_readfirstlane(d.first_blk);
   if (blk < 0 || blk >= __builtin_amdgcn_readfirstlane(d.fa.nblk)) return;
   const Ctrl c = load_ctrl_uniform(d.ctrl);
-  if (!c.done || !c.accepted) return;
+  const uint32_t* fa_words = (const uint32_t*)&d.fa;
+  if (!c.done || !c.accepted) {  // an unfinished stream (later rounds) or the re-init branch
+    if (blk == 0) owners_no_resample<T, RNG, MAXM, SP>(d.fa, fa_words, c, d.ctrl, d.prior, d.mlpose, d.out, d.seq, nullptr, sh);
+    return;
+  }
   const __amdgpu_buffer_rsrc_t ors =
       __builtin_amdgcn_make_buffer_rsrc((void*)d.fa.owner_out, (short)0, d.fa.N * 4, 0x00020000);
   double carry_R = __longlong_as_double(0x7ff8dead00000000ll);
   int carry_hi = 0;
   unsigned long long key = 0ull;
-  resample_owners_block<T, RNG, SP>(d.fa, (const uint32_t*)&d.fa, blk, c, d.prior, c.kept_slot ? d.w1 : d.w0, ors,
-                                    c.kept_slot ? d.bscan1 : d.bscan0, d.gscan, d.counts, d.mlpose, sh, carry_R,
-                                    carry_hi, key, [](unsigned long long) {});
-  if (lane_id() == 0)  // every block has a valid particle, so a key (count 0 included): win_key decoded
-    d.cpart[blk] = CountPart{(int32_t)(key >> 32), 0x7fffffff - (int32_t)(uint32_t)key};
+  unsigned long long* winkey = d.winkey;
+  const bool finisher = blk == __builtin_amdgcn_readfirstlane(d.fa.nblk) - 1;
+  resample_owners_block<T, RNG, SP>(d.fa, fa_words, blk, c, d.prior, c.kept_slot ? d.w1 : d.w0, ors,
+                                    c.kept_slot ? d.bscan1 : d.bscan0, d.gscan, d.counts, d.mlpose, sh.o, carry_R,
+                                    carry_hi, key, [&](unsigned long long k) {
+                                      if (k && lane_id() == 0)
+                                        __hip_atomic_fetch_max(winkey + (blk & (kWinShards - 1)) * kWinStride, k,
+                                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                      if (!finisher && lane_id() == 0)
+                                        (void)__hip_atomic_fetch_add(
+                                            win_arrive(winkey) + (blk & (kWinShards - 1)) * kArriveStride, 1u,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    });
+  if (!finisher) return;
+  owners_finish<T, RNG, MAXM, SP>(d.fa, fa_words, c, d.ctrl, d.prior, d.table, d.mlpose, winkey, d.out, d.seq, nullptr,
+                                  sh);
 }
 
 // ---- launch 3 of the two-launch path (one block): winner = argmax of the block count partials (first

@@ -782,7 +782,8 @@ struct Seq {
         {offsetof(Desc, gcount_r), "gcount_r"}, {offsetof(Desc, tcount_r), "tcount_r"}, {offsetof(Desc, prop0), "prop0"},
         {offsetof(Desc, prop1), "prop1"},   {offsetof(Desc, cpart), "cpart"},   {offsetof(Desc, cgroup), "cgroup"},
         {offsetof(Desc, counts), "counts"}, {offsetof(Desc, cand), "cand"},     {offsetof(Desc, mlpose), "mlpose"},
-        {offsetof(Desc, out), "out"},       {offsetof(Desc, seq), "seq|first_blk"}, {offsetof(Desc, gen), "gen"},
+        {offsetof(Desc, out), "out"},       {offsetof(Desc, winkey), "winkey"},
+        {offsetof(Desc, seq), "seq|first_blk"}, {offsetof(Desc, gen), "gen"},
         {offsetof(Desc, tag), "tag"},       {offsetof(FrameArgsT<T>, key0), "fa.key0|key1"},
         {offsetof(FrameArgsT<T>, flo), "fa.flo|fhi"}};
     auto name = [&](size_t off) -> std::string {
@@ -880,6 +881,7 @@ struct Seq {
         x.cand = c->d_cand;
         x.mlpose = c->d_mlpose;
         x.out = c->d_out;
+        x.winkey = c->d_winkey;
         c->seq = (c->seq + 1) & 0x3fffffff;
         x.seq = c->seq;
         x.first_blk = (int32_t)total;
@@ -1000,10 +1002,11 @@ struct Seq {
         cs[act[i]]->last_resample =
             all_owners && !(c0->diag & kDiagBlockResample) ? PFMPE_RESAMPLE_OWNERS : PFMPE_RESAMPLE_BLOCKS;
       }
+      const bool owners = all_owners && !(c0->diag & kDiagBlockResample);
       RET(launch_ext(c0, PFMPE_K_RESAMPLE, [&] {
-        if (all_owners && !(c0->diag & kDiagBlockResample))  // a wave per block (§4.2d)
-          klaunch(c0, k_resample_owners_multi<T, RNG, SP>, dim3((unsigned)((total + kWaves - 1) / kWaves)), dim3(kBlock),
-                  0, dd, db, na, (const uint32_t*)dstat, gen, (int)total);
+        if (owners)  // a wave per block (§4.2d), each stream finished by its last block's wave
+          klaunch(c0, k_resample_owners_multi<T, RNG, MAXM, SP>, dim3((unsigned)((total + kWaves - 1) / kWaves)),
+                  dim3(kBlock), 0, dd, db, na, (const uint32_t*)dstat, gen, (int)total);
         else if (all_kept)
           klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, true>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
                   (const uint32_t*)dstat, gen);
@@ -1011,10 +1014,11 @@ struct Seq {
           klaunch(c0, k_resample_multi<T, RNG, MAXM, SP, false>, dim3((unsigned)total), dim3(kBlock), 0, dd, db, na,
                   (const uint32_t*)dstat, gen);
       }));
-      RET(launch_ext(c0, PFMPE_K_FINAL, [&] {
-        klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd,
-                (const uint32_t*)dstat, gen);
-      }));
+      if (!owners)
+        RET(launch_ext(c0, PFMPE_K_FINAL, [&] {
+          klaunch(c0, k_resample_final_multi<T, RNG, MAXM, SP>, dim3((unsigned)na), dim3(kFinalBlock), lds_f, dd,
+                  (const uint32_t*)dstat, gen);
+        }));
       const int64_t t_l1 = now_ns();
       c0->mt_ns[1] += t_l1 - t_l0;
       std::vector<int> next;
