@@ -2068,10 +2068,8 @@ __device__ __forceinline__ GroupScan load_gscan_wt(const GroupScan* p) {
 // W4 (k_group after the streaming pass): `part` holds kWaves wave partials per block (BlockPart fields: wave
 // total, max / min in-wave prefix, max / argmax, min / argmin), combined here into the block partial with
 // publish_iteration's association (((0 + t0) + t1) + ..., the running extrema of pre + prefix, waves in order).
-// W4: the partials are wave partials (four per block, the streaming passes); SC1 (with W4): written in this launch
-// by other waves (8-B agent-scope stores, drained before their arrivals: the fused tail of the packed passes), so
-// read with 8-B agent-scope loads (MI355X_MICROARCH.md "Valid forms": 8-B agent atomics both sides)
-template <bool W4 = false, bool SC1 = false>
+// W4: the partials are wave partials (four per block, the streaming passes)
+template <bool W4 = false>
 __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, const BlockPart* __restrict__ part,
                                                      BlockScan* __restrict__ bscan, GroupPart* __restrict__ gpart) {
   const int lane = lane_id();
@@ -2087,22 +2085,8 @@ __device__ __forceinline__ GroupPart propagate_group(int nblk, int gsz, int g, c
     if (vb && W4) {  // written by the previous launch: plain loads
       const BlockPart* p = part + (size_t)b * kWaves;
       BlockPart w[kWaves];
-      if constexpr (SC1) {
 #pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) {
-          w[ww].sum = ld_wt_d(&p[ww].sum);
-          w[ww].maxrel = ld_wt_d(&p[ww].maxrel);
-          w[ww].minrel = ld_wt_d(&p[ww].minrel);
-          w[ww].maxw = ld_wt_d(&p[ww].maxw);
-          w[ww].minw = ld_wt_d(&p[ww].minw);
-          const uint64_t ai = ld_wt(&p[ww].argmax);
-          w[ww].argmax = lo32(ai);
-          w[ww].argmin = hi32(ai);
-        }
-      } else {
-#pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) w[ww] = p[ww];
-      }
+      for (int ww = 0; ww < kWaves; ++ww) w[ww] = p[ww];
       double pre = 0.0, bmx = w[0].maxw, bmn = w[0].minw;
       int bix = w[0].argmax, bin = w[0].argmin;
 #pragma unroll

@@ -226,8 +226,6 @@ __device__ __forceinline__ void grid_walk(const unsigned char* ents, uint32_t re
 //    argmin = none}.
 // Anything else (a partial wave past N, a negative weight) takes wave_weight_partials as k_weigh_stream does.
 // full: every particle of the task is below N (wave-uniform, decided on the scalar unit: no validity ballots).
-// WT: every word as an 8-B agent-scope store (the fused tail reads the partials in this launch: PkTail)
-template <bool WT = false>
 __device__ __forceinline__ void pk_wave_partial(float w, bool valid, bool full, int nbase, BlockPart* __restrict__ dst) {
   const int lane = lane_id();
   if (full && __builtin_amdgcn_ballot_w64(w < 0.0f) == 0) {
@@ -259,29 +257,16 @@ __device__ __forceinline__ void pk_wave_partial(float w, bool valid, bool full, 
     } else {
       wi = wave_total_lane63(x);
     }
-    if constexpr (WT) {
-      if (lane == 63) {
-        st_wt_d(&dst->sum, wi);
-        st_wt_d(&dst->maxrel, wi);
-      }
-      if (lane == 0) {
-        st_wt_d(&dst->minrel, x);
-        st_wt_d(&dst->maxw, (double)__int_as_float(mxb));
-        st_wt_d(&dst->minw, (double)INFINITY);
-        st_wt(&dst->argmax, pack2(ix, 0x7fffffff));
-      }
-    } else {
-      if (lane == 63) {
-        dst->sum = wi;
-        dst->maxrel = wi;
-      }
-      if (lane == 0) {
-        dst->minrel = x;
-        dst->maxw = (double)__int_as_float(mxb);
-        dst->minw = (double)INFINITY;
-        dst->argmax = ix;
-        dst->argmin = 0x7fffffff;
-      }
+    if (lane == 63) {
+      dst->sum = wi;
+      dst->maxrel = wi;
+    }
+    if (lane == 0) {
+      dst->minrel = x;
+      dst->maxw = (double)__int_as_float(mxb);
+      dst->minw = (double)INFINITY;
+      dst->argmax = ix;
+      dst->argmin = 0x7fffffff;
     }
     return;
   }
@@ -291,57 +276,16 @@ __device__ __forceinline__ void pk_wave_partial(float w, bool valid, bool full, 
   wave_weight_partials(w, valid, nbase + lane, wi, rmx, rmn, mx, ix, mn, in_);
   const double tot = lane_value(wi, 63);
   if (lane == 0) {
-    if constexpr (WT) {
-      st_wt_d(&dst->sum, tot);
-      st_wt_d(&dst->maxrel, rmx);
-      st_wt_d(&dst->minrel, rmn);
-      st_wt_d(&dst->maxw, (double)mx);
-      st_wt_d(&dst->minw, (double)mn);
-      st_wt(&dst->argmax, pack2(ix, in_));
-    } else {
-      BlockPart q;
-      q.sum = tot;
-      q.maxrel = rmx;
-      q.minrel = rmn;
-      q.maxw = (double)mx;
-      q.minw = (double)mn;
-      q.argmax = ix;
-      q.argmin = in_;
-      *dst = q;
-    }
+    BlockPart q;
+    q.sum = tot;
+    q.maxrel = rmx;
+    q.minrel = rmn;
+    q.maxw = (double)mx;
+    q.minw = (double)mn;
+    q.argmax = ix;
+    q.argmin = in_;
+    *dst = q;
   }
-}
-
-// ---- the group / top hand-off inside the one-stream packed passes (round 6, VERDICT r05 item 3: no k_group_top /
-// k_group + k_top_wide launch after k_weigh_pk / k_weigh_pk12).  A group is 2 * gsz tasks.  After a task's two wave
-// partials (8-B agent-scope stores), the wave arrives on its group's counter, deferred: the drain and the add go at
-// the next task's first memory wait (after its generator, where the wave waits for its prefetched state anyway), and
-// the add's return value is read at the end of that task, long after it came back.  The arrival that completes a
-// group (the value 2 * nb - 1) makes its wave the group's reducer: propagate_group over the group's wave partials
-// (8-B agent loads), the block scans and the group partial written through, then an arrival on the top counter, and
-// the last group runs propagate_top, which writes the control record and the group scans k_resample_owners reads.
-// The same functions and associations as k_group_top / k_group + k_top, so every output is unchanged (the serial
-// tiles of propagate_top where k_top_wide spread them over 16 waves: identical sums and maxima).  A wave's last task
-// arrives after its loop.
-struct PkTail {
-  BlockScan* bscan[2];
-  GroupPart* gpart[2];
-  GroupScan* gscan;
-  uint32_t* gcount;  // ngrp group counters, zero between launches
-  uint32_t* tcount;  // the top counter
-  Ctrl* ctrl;
-};
-__device__ __forceinline__ int pk_group_tasks(const FrameArgsT<float>& fa, int g) {
-  return 2 * min(fa.gsz, fa.nblk - g * fa.gsz);
-}
-// the group's reduction and, for the last group, the top (one wave); the caller's add returned old for group g
-__device__ __forceinline__ void pk_group_top(const FrameArgsT<float>& fa, const PkTail* __restrict__ tl,
-                                             const BlockPart* __restrict__ parts, int slot, int g, int iter) {
-  const GroupPart gr = propagate_group<true, true>(fa.nblk, fa.gsz, g, parts, tl->bscan[slot], tl->gpart[slot]);
-  const bool single = fa.ngrp == 1;
-  if (!single && !wave_arrive_last(tl->tcount, fa.ngrp)) return;
-  propagate_top<float, kRngPhilox>(fa, tl->ctrl, iter, tl->gpart[0], tl->gpart[1], tl->gscan, nullptr, 0u, gr, single,
-                                   slot);
 }
 
 // Per-block LDS copies of the frame constants the loop reads besides LdsConst (the anchors and the grid's float
