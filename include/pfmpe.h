@@ -338,7 +338,7 @@ enum { PFMPE_OPT_RECORD_COUNTS = 1, PFMPE_OPT_PRUNE = 2, PFMPE_OPT_TIMING = 3, P
 int pfmpe_set_option(pfmpe_ctx* ctx, int option, int64_t value);
 
 /* Context state for monitoring and tests (no reference counterpart: engine introspection). */
-enum { PFMPE_SHAPE_TWO_LAUNCH = 0, /* k_propagate_weigh (+ re-launches) + k_resample + k_resample_final */
+enum { PFMPE_SHAPE_TWO_LAUNCH = 0, /* weighing pass (+ re-launches) + hand-off + resampling (+ final)   */
        PFMPE_SHAPE_FRAME = 1,      /* k_frame: one launch, tree hand-offs                                */
        PFMPE_SHAPE_FRAME2 = 2 };   /* k_frame2: one launch, flat hand-offs                               */
 enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 after a fallback)       */
@@ -353,11 +353,12 @@ enum { PFMPE_INFO_FUSED = 1,            /* current one-launch mode (0/1/2; 0 aft
 /* The two-launch shape's weighing pass: one block per 256 particles (k_propagate_weigh), or
  * resident blocks streaming over them with the next block's state prefetched (k_weigh_stream + k_group +
  * k_top), or the streaming pass with two particles per lane in packed fp32 (k_weigh_pk: 5 markers, fp32 / fp16
- * state, the Philox stream, the blob grid).  All give bit-identical results. */
+ * state; k_weigh_pk12: 12 markers, fp32 state; the Philox stream, the blob grid).  All give bit-identical
+ * results. */
 enum { PFMPE_WEIGH_BLOCKS = 0, PFMPE_WEIGH_STREAM = 1, PFMPE_WEIGH_PK = 2 };
 /* The two-launch shape's resampling launch: one block per 256 particles with the new prior materialised
  * (k_resample, then k_resample_final), or, for a deferred frame, one wave per 256-particle block writing owner
- * indices whose last wave finishes the frame (k_resample_owners; DESIGN.md §4.2d).  Same outputs. */
+ * indices whose last wave finishes the frame (k_resample_owners; DESIGN.md §4.2d, §4.2e).  Same outputs. */
 enum { PFMPE_RESAMPLE_BLOCKS = 0, PFMPE_RESAMPLE_OWNERS = 1 };
 int pfmpe_get_info(const pfmpe_ctx* ctx, int key, int64_t* value);
 
@@ -370,11 +371,11 @@ int pfmpe_stage_blob_bank(pfmpe_ctx* ctx, const double* blobs, const int32_t* of
 /* Per-kernel statistics collected while PFMPE_OPT_TIMING is on: launches and summed device time (ms)
  * measured with HIP events on the ctx stream. */
 enum { PFMPE_K_PROPAGATE = 0, /* k_propagate_weigh (+ last-block iteration reduce)  */
-       PFMPE_K_RESAMPLE = 1,  /* k_resample: resampling + block count partials       */
-       PFMPE_K_AUX = 2,       /* regeneration for pfmpe_get_particles                */
+       PFMPE_K_RESAMPLE = 1,  /* k_resample / k_resample_owners: resampling           */
+       PFMPE_K_AUX = 2,       /* hand-off kernels (k_group*, k_top*), regeneration   */
        PFMPE_K_FRAME = 3,     /* k_frame: the whole frame in one launch              */
        PFMPE_K_ROI = 4,       /* k_roi + k_roi_final (pfmpe_predict_roi)             */
-       PFMPE_K_FINAL = 5,     /* k_resample_final: winner + frame record (one block) */
+       PFMPE_K_FINAL = 5,     /* k_resample_final (non-deferred frames): the record   */
        PFMPE_K_P3P_HIST = 6,  /* k_p3p_hist: initialisation histogram                */
        PFMPE_K_P3P_CHECK = 7, /* k_p3p_check: checkCorrespondences of all candidates */
        PFMPE_K_DETECT = 8,    /* k_det_*: the LED detector pipeline (pfmpe_find_leds) */
