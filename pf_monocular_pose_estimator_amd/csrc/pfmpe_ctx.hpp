@@ -84,7 +84,7 @@ struct pfmpe_ctx {
   GroupPart* d_gpart[2] = {nullptr, nullptr};
   GroupScan* d_gscan = nullptr;
   CountPart* d_cpart = nullptr;
-  unsigned long long* d_winkey = nullptr;  // kWinShards winner keys (k_resample -> k_resample_final), zero between frames
+  unsigned long long* d_winkey = nullptr;  // kWinShards winner keys + the owners finish's arrival shards (kWinBytes), zero between frames
   CountPart* d_cgroup = nullptr;
   uint32_t* d_counters = nullptr;  // [prop group x max_grp][prop top][res group x max_grp][res top]
   uint32_t* d_gen = nullptr;       // k_frame iteration release word (monotonic)
@@ -475,6 +475,19 @@ inline const void* pk_kernel() {
     return nullptr;
 }
 
+// A two-launch frame or batch that left no record (a bounded wait expired, or a HIP error): the control record, the
+// winner keys, the fused finish's arrival shards and the hand-off counters may hold the failed frame's partial state,
+// which the next frame would take as its own (the control record's iteration state; a finisher that stops polling
+// early).  Zero them once `on` has drained, as abandoned() does for a one-launch frame; the prior is untouched.
+inline int reset_handoffs(pfmpe_ctx* c, hipStream_t on) {
+  HIPCHK(c, hipStreamSynchronize(on));
+  HIPCHK(c, hipMemsetAsync(c->d_ctrl, 0, sizeof(Ctrl), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_counters, 0, counters_bytes(c), c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_winkey, 0, kWinBytes, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PFMPE_OK;
+}
+
 // A one-launch frame abandoned by a bounded wait (blocks not co-resident: other work on the device): clear the
 // hand-off state, stop fusing on this context; the caller redoes the frame with two launches.
 inline int abandoned(pfmpe_ctx* c) {
@@ -646,7 +659,11 @@ struct Seq {
                 c->d_ctrl, table, prior, c->d_cpart, c->d_cand, c->d_mlpose, c->d_out, seq, c->d_stamps, kept ? 1 : 0,
                 c->d_winkey);
       }));
-    RET(wait_frame(c));
+    if (const int rc = wait_frame(c); rc != PFMPE_OK) {
+      const std::string err = c->err;
+      (void)reset_handoffs(c, c->stream);
+      return fail(c, rc, err);
+    }
     return PFMPE_OK;
   }
   // the whole frame as one launch, if every block can be resident at once: k_frame2 (flat hand-offs,
@@ -1024,8 +1041,11 @@ struct Seq {
       std::vector<int> next;
       for (int i = 0; i < na; ++i) {
         pfmpe_ctx* c = cs[act[i]];
-        if (wait_frame(c, c0->stream) != PFMPE_OK)
-          return batch_failure(c0, cs, act, want, d + Lt.doff, dstat, gen, c->err);
+        if (wait_frame(c, c0->stream) != PFMPE_OK) {
+          const std::string err = c->err;
+          for (int k = 0; k < na; ++k) (void)reset_handoffs(cs[act[k]], c0->stream);
+          return batch_failure(c0, cs, act, want, d + Lt.doff, dstat, gen, err);
+        }
         if (!frame_done(c)) next.push_back(act[i]);
       }
       c0->mt_ns[2] += now_ns() - t_l1;

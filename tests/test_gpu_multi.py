@@ -442,3 +442,36 @@ def test_multi_streaming_pk_batch_equals_single_streams(state):
             (777, 5, 20, False, "")]
     _check_batch(state, pf.RNG_PHILOX, 3, cfgs, passes_out=(passes := []))
     assert passes and all(p == pf.WEIGH_PK for p in passes), passes
+
+
+def test_multi_abandoned_finish_leaves_no_state():
+    """A batch in which one stream's finishing wave gives up (that context's PFMPE_DIAG 128) fails as a whole
+    (no record for that stream); every stream's keys and arrival shards are zeroed, and the next batch, on different
+    frames, equals solo engines that never saw the failed batch."""
+    cfgs = [(100_000, 5, 50, False, ""), (4099, 5, 50, False, "")]
+    streams = _streams(3, cfgs)
+    batch, solo = [], []
+    for (st, frames, how), (N, M, *_rest) in zip(streams, cfgs):
+        for lst in (batch, solo):
+            e = _engine(N, M, pf.STATE_F32, pf.RNG_PHILOX, fused=0)
+            e.set_prior(st.prior(N))
+            lst.append(e)
+    try:
+        def ins_for(engs, f):
+            return [_frame(engs[s], streams[s][1][f][0], streams[s][1][f][1], "", 1000 + 17 * s + f, f)
+                    for s in range(len(streams))]
+        pf.Engine.step_multi(batch, ins_for(batch, 0))
+        for s in range(len(streams)):
+            solo[s].step(ins_for(solo, 0)[s])
+        batch[1].set_option(pf.OPT_DIAG, pf.DIAG_ABANDON)
+        with pytest.raises(pf.PFError):
+            pf.Engine.step_multi(batch, ins_for(batch, 1))
+        batch[1].set_option(pf.OPT_DIAG, 0)
+        outs = pf.Engine.step_multi(batch, ins_for(batch, 2))
+        assert batch[0].info(pf.INFO_LAST_RESAMPLE) == pf.RESAMPLE_OWNERS
+        for s in range(len(streams)):
+            ref = solo[s].step(ins_for(solo, 2)[s])
+            _same(_snapshot(batch[s], outs[s]), _snapshot(solo[s], ref), ("after abandon", s))
+    finally:
+        for e in batch + solo:
+            e.close()

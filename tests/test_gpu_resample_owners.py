@@ -202,3 +202,34 @@ def test_owners_dominant_particles(state, N, doms):
     assert counts.max() > 256 and (N < (1 << 23) or counts.max() >= (1 << 23))
     assert a[0]["out"]["winner_idx"] == int(np.argmax(counts))
     _assert_same(a, b)
+
+
+def test_owners_abandoned_finish_leaves_no_state():
+    """A two-launch frame whose finishing wave gives up (PFMPE_DIAG 128, as if the wait bound expired) returns an
+    error without a record and leaves the winner keys and arrival shards set; the host zeroes them
+    (reset_handoffs, pfmpe_ctx.hpp), so the next frame, a different one, equals the same frame on an engine that
+    never saw the failure (its finisher would otherwise stop polling early and count the failed frame's keys)."""
+    N = 100_003
+    st = syn.make_stream(syn.StreamConfig("t", M=5, B=50, N=N), 3)
+    frames = _frames(st, occlude_second=False)
+    runs = []
+    for fail_second in (True, False):
+        eng = make_engine(N, st.markers, st.K, pf.STATE_F32, pf.RNG_PHILOX, fused=0)
+        eng.set_prior(st.prior(fast=True))
+        try:
+            def step(f):
+                cur, pred, predm, blobs, dt, kw = frames[f]
+                return eng.step(eng.make_frame(cur, pred, predm, blobs=blobs, dt=dt, seed=808 + f, frame_idx=f,
+                                               **kw)).as_dict()
+            step(0)
+            if fail_second:
+                eng.set_option(pf.OPT_DIAG, pf.DIAG_ABANDON)
+                with pytest.raises(pf.PFError, match="record"):
+                    step(1)
+                assert eng.info(pf.INFO_LAST_RESAMPLE) == pf.RESAMPLE_OWNERS
+                eng.set_option(pf.OPT_DIAG, 0)
+            out = step(2)
+            runs.append([{"out": out, "w": eng.get_weights(), "p1": eng.get_particles(1), "counts": eng.get_counts()}])
+        finally:
+            eng.close()
+    _assert_same(runs[0], runs[1])
