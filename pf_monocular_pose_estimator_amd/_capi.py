@@ -25,6 +25,7 @@ OPT_WAIT_BOUND_US, OPT_FUSED_REARM, OPT_MULTI_MAX_BLOCKS = 6, 7, 8
 OPT_DIAG = 99  # undocumented diagnostic switches (csrc/pf_kernels.hpp kDiag*)
 DIAG_LAG_LOADS, DIAG_ABANDON, DIAG_NO_STREAM, DIAG_FORCE_STREAM, DIAG_SERIAL_TOP = 64, 128, 512, 1024, 2048
 DIAG_NO_PK, DIAG_CORRUPT_DESC, DIAG_NO_DEFER, DIAG_BLOCK_RESAMPLE, DIAG_MIN_SIDE = 4096, 8192, 16384, 32768, 65536
+DIAG_ABANDON_FINISH = 131072
 OPT_DEFER_RESAMPLE = 9
 SHAPE_TWO_LAUNCH, SHAPE_FRAME, SHAPE_FRAME2 = 0, 1, 2
 INFO_FUSED, INFO_FUSED_FALLBACKS, INFO_LAST_SHAPE, INFO_GUARD_SKIPS, INFO_N, INFO_LAST_WEIGH_PASS = 1, 2, 3, 4, 5, 6

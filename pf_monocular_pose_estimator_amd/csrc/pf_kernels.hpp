@@ -1641,8 +1641,7 @@ enum : int {
   kDiagTreeCount = 16,  // k_frame: count barrier as a tree instead of flat
   kDiagSqrtGroups = 32, // groups of ~sqrt(nblk) blocks even when the frame fits k_frame2
   kDiagLagLoads = 64,   // k_frame2: the last block sleeps ~20 us before loading the block partials
-  kDiagAbandon = 128,   // k_frame2: every block gives up its first weighing-barrier wait; k_resample_owners(_multi):
-                        // the finishing wave gives up before polling the arrivals (recovery tests)
+  kDiagAbandon = 128,   // k_frame2: every block gives up its first weighing-barrier wait (recovery test)
   kDiagSortedScore = 256, // fp32: the sorted (extraction-order) score even when B >= M (A/B of score_unordered)
   kDiagNoStream = 512,     // two-launch path: never the streaming weighing pass (k_weigh_stream + k_group + k_top)
   kDiagForceStream = 1024, // two-launch path: always the streaming weighing pass (tests / A/B)
@@ -1652,6 +1651,8 @@ enum : int {
                            // staging check; the altered word is a key word, never a pointer)
   kDiagNoDefer = 16384,    // two-launch frames materialise the new prior even with the kept set (A/B of deferral)
   kDiagMinSide = 65536,      // k_frame2: run the zmin scans (group_zmin2) even when no weight can be negative (tests)
+  kDiagAbandonFinish = 131072,  // k_resample_owners(_multi): the finishing wave gives up before polling the arrivals
+                                // (the two-launch recovery tests)
   kDiagBlockResample = 32768  // deferred two-launch frames resample with the block-per-256 k_resample instead of
                               // k_resample_owners' wave per 256 (A/B, identity tests)
 };
@@ -4079,7 +4080,7 @@ __device__ __forceinline__ void owners_finish(const FrameArgsT<T>& fa, const uin
                                               int32_t seq, uint64_t* __restrict__ stamps, OwnersFinalLds<T>& sh) {
   const int lane = lane_id();
   static_assert(kWinShards == 64, "one shard per lane");
-  if (fa.diag & kDiagAbandon) return;  // as if the wait bound expired: no record, keys and arrivals left set
+  if (fa.diag & kDiagAbandonFinish) return;  // as if the wait bound expired: no record, keys and arrivals left set
   {  // every other block's arrival (the blocks b < nblk - 1 with b % 64 == lane)
     uint32_t* sh_arrive = win_arrive(winkey) + lane * kArriveStride;
     const uint32_t want = lane < fa.nblk - 1 ? (uint32_t)((fa.nblk - 2 - lane) / 64 + 1) : 0u;

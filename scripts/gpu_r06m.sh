@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6 (m): the whole -m gpu suite and smoke() on the tree after the fused hand-off was rejected
+# Round 6 (m): the whole -m gpu suite and smoke() (run again on the final tree)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out/r06; export TMPDIR=/tmp
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r06/gpu_suite_m.log 2>&1; r=$?

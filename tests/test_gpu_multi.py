@@ -445,7 +445,7 @@ def test_multi_streaming_pk_batch_equals_single_streams(state):
 
 
 def test_multi_abandoned_finish_leaves_no_state():
-    """A batch in which one stream's finishing wave gives up (that context's PFMPE_DIAG 128) fails as a whole
+    """A batch in which one stream's finishing wave gives up (that context's PFMPE_DIAG 131072) fails as a whole
     (no record for that stream); every stream's keys and arrival shards are zeroed, and the next batch, on different
     frames, equals solo engines that never saw the failed batch."""
     cfgs = [(100_000, 5, 50, False, ""), (4099, 5, 50, False, "")]
@@ -463,7 +463,7 @@ def test_multi_abandoned_finish_leaves_no_state():
         pf.Engine.step_multi(batch, ins_for(batch, 0))
         for s in range(len(streams)):
             solo[s].step(ins_for(solo, 0)[s])
-        batch[1].set_option(pf.OPT_DIAG, pf.DIAG_ABANDON)
+        batch[1].set_option(pf.OPT_DIAG, pf.DIAG_ABANDON_FINISH)
         with pytest.raises(pf.PFError):
             pf.Engine.step_multi(batch, ins_for(batch, 1))
         batch[1].set_option(pf.OPT_DIAG, 0)

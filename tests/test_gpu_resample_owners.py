@@ -205,7 +205,7 @@ def test_owners_dominant_particles(state, N, doms):
 
 
 def test_owners_abandoned_finish_leaves_no_state():
-    """A two-launch frame whose finishing wave gives up (PFMPE_DIAG 128, as if the wait bound expired) returns an
+    """A two-launch frame whose finishing wave gives up (PFMPE_DIAG 131072, as if the wait bound expired) returns an
     error without a record and leaves the winner keys and arrival shards set; the host zeroes them
     (reset_handoffs, pfmpe_ctx.hpp), so the next frame, a different one, equals the same frame on an engine that
     never saw the failure (its finisher would otherwise stop polling early and count the failed frame's keys)."""
@@ -223,7 +223,7 @@ def test_owners_abandoned_finish_leaves_no_state():
                                                **kw)).as_dict()
             step(0)
             if fail_second:
-                eng.set_option(pf.OPT_DIAG, pf.DIAG_ABANDON)
+                eng.set_option(pf.OPT_DIAG, pf.DIAG_ABANDON_FINISH)
                 with pytest.raises(pf.PFError, match="record"):
                     step(1)
                 assert eng.info(pf.INFO_LAST_RESAMPLE) == pf.RESAMPLE_OWNERS
