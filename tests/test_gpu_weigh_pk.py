@@ -166,3 +166,18 @@ def test_pk_pass_default_at_c4_c5():
             assert eng.info(pf.INFO_LAST_WEIGH_PASS) == pf.WEIGH_PK, name
         finally:
             eng.close()
+
+
+@pytest.mark.parametrize("M,B,heavy", [(5, 50, False), (12, 200, True)])
+@pytest.mark.parametrize("N", [3, 129, 4_099])
+def test_pk_passes_small_n(M, B, heavy, N):
+    """Tiny particle counts through the packed passes (forced streaming): a task holding particles 0 and 1 (the
+    current / predicted poses, PE:547-551) with almost every lane past N, a second task with none, one partial wave
+    (129), and a partial last block (4,099); steady / 80-iteration / it_since_init = 1 frames, fp32 state."""
+    st = syn.make_stream(syn.StreamConfig("t", M=M, B=B, N=N, heavy=heavy), 3)
+    frames = _frames(st)
+    frames[1] = (frames[1][0], frames[1][1], {"force_iters": 80})
+    a, pa = _run(st, N, pf.STATE_F32, pf.DIAG_FORCE_STREAM, frames)
+    b, pb = _run(st, N, pf.STATE_F32, pf.DIAG_FORCE_STREAM | pf.DIAG_NO_PK, frames)
+    assert pa == [pf.WEIGH_PK] * 3 and pb == [pf.WEIGH_STREAM] * 3, (pa, pb)
+    _assert_same(a, b)
